@@ -1,0 +1,293 @@
+"""ctypes binding of liblidarsm.so (include/lidarsm.h).
+
+The shared library is built in-tree (``lidar_slam_arvc_amd/_lib/liblidarsm.so``) by
+``__graft_entry__.build()`` / ``make -C lidar_slam_arvc_amd/csrc``. There is no CPU fallback: if
+the library or a gfx950 device is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "liblidarsm.so")
+
+LSM_OK = 0
+LSM_P2P = 0
+LSM_P2PLANE = 1
+
+EXPORTED = [
+    "lsm_init", "lsm_free", "lsm_last_error", "lsm_version", "lsm_default_prep_params",
+    "lsm_default_icp_params", "lsm_cloud_upload", "lsm_cloud_upload_f64", "lsm_cloud_release",
+    "lsm_cloud_info", "lsm_preprocess", "lsm_preprocess_batch", "lsm_cloud_download",
+    "lsm_cloud_voxel_keys", "lsm_icp", "lsm_icp_batch", "lsm_icp_last_correspondences",
+    "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
+    "lsm_reset_stats",
+]
+
+
+class PrepParams(C.Structure):
+    _fields_ = [("min_radius", C.c_double), ("max_radius", C.c_double),
+                ("min_height", C.c_double), ("max_height", C.c_double),
+                ("voxel_size", C.c_double), ("normal_radius", C.c_double),
+                ("max_nn", C.c_int32), ("want_normals", C.c_int32),
+                ("grid_cell", C.c_double)]
+
+
+class IcpParams(C.Structure):
+    _fields_ = [("max_correspondence_distance", C.c_double), ("method", C.c_int32),
+                ("max_iteration", C.c_int32), ("relative_fitness", C.c_double),
+                ("relative_rmse", C.c_double)]
+
+
+class IcpResult(C.Structure):
+    _fields_ = [("transformation", C.c_double * 16), ("fitness", C.c_double),
+                ("inlier_rmse", C.c_double), ("correspondences", C.c_int64),
+                ("iterations", C.c_int32), ("status", C.c_int32)]
+
+
+_P = C.c_void_p
+_i64p = C.POINTER(C.c_int64)
+_f64p = C.POINTER(C.c_double)
+_f32p = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int32)
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise RuntimeError(f"liblidarsm.so not found at {path}; build it with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(path)
+    sig = {
+        "lsm_init": (C.c_int, [C.c_int, C.POINTER(_P)]),
+        "lsm_free": (C.c_int, [_P]),
+        "lsm_last_error": (C.c_char_p, [_P]),
+        "lsm_version": (C.c_char_p, []),
+        "lsm_default_prep_params": (None, [C.POINTER(PrepParams)]),
+        "lsm_default_icp_params": (None, [C.POINTER(IcpParams)]),
+        "lsm_cloud_upload": (C.c_int, [_P, _f32p, C.c_int64, _i64p]),
+        "lsm_cloud_upload_f64": (C.c_int, [_P, _f64p, C.c_int64, _i64p]),
+        "lsm_cloud_release": (C.c_int, [_P, C.c_int64]),
+        "lsm_cloud_info": (C.c_int, [_P, C.c_int64, _i64p, _i64p, _i32p]),
+        "lsm_preprocess": (C.c_int, [_P, C.c_int64, C.POINTER(PrepParams), _i64p]),
+        "lsm_preprocess_batch": (C.c_int, [_P, C.c_int64, _i64p, C.POINTER(PrepParams), _i64p]),
+        "lsm_cloud_download": (C.c_int, [_P, C.c_int64, _f64p, _f64p, C.c_int64]),
+        "lsm_cloud_voxel_keys": (C.c_int, [_P, C.c_int64, _i32p, C.c_int64]),
+        "lsm_icp": (C.c_int, [_P, C.c_int64, C.c_int64, _f64p, C.POINTER(IcpParams),
+                              C.POINTER(IcpResult)]),
+        "lsm_icp_batch": (C.c_int, [_P, C.c_int64, _i64p, _i64p, _f64p, C.POINTER(IcpParams),
+                                    C.POINTER(IcpResult)]),
+        "lsm_icp_last_correspondences": (C.c_int, [_P, _i64p, C.c_int64, _i64p]),
+        "lsm_loop_candidates": (C.c_int, [_P, _f64p, C.c_int64, C.c_double, C.c_double, _i64p,
+                                          _i64p, C.c_int64, _i64p]),
+        "lsm_loop_triplet_partners": (C.c_int, [_P, _f64p, C.c_int64, _i64p, C.c_int64, _i64p]),
+        "lsm_set_timing": (C.c_int, [_P, C.c_int32]),
+        "lsm_kernel_stats": (C.c_int, [_P, C.c_char_p, _i64p, _f64p, _f64p]),
+        "lsm_reset_stats": (C.c_int, [_P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib() -> C.CDLL:
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            _lib = load_library()
+        return _lib
+
+
+def _ptr(a: np.ndarray, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+class Device:
+    """One liblidarsm context (one GPU). Use :func:`device` for the per-process default."""
+
+    def __init__(self, index: int = 0):
+        self.lib = lib()
+        h = _P()
+        rc = self.lib.lsm_init(int(index), C.byref(h))
+        if rc != LSM_OK:
+            raise RuntimeError(f"lsm_init({index}) failed with code {rc}: no usable gfx950 device "
+                               "(the registration path has no CPU fallback)")
+        self.handle = h
+        self.index = index
+
+    # -- errors ------------------------------------------------------------------------------
+    def check(self, rc: int, what: str):
+        if rc != LSM_OK:
+            msg = self.lib.lsm_last_error(self.handle).decode()
+            raise RuntimeError(f"{what}: {msg} (code {rc})")
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.lsm_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- clouds ------------------------------------------------------------------------------
+    def upload(self, points) -> int:
+        p = np.asarray(points)
+        if p.ndim != 2 or p.shape[1] != 3:
+            raise ValueError("points must be N x 3")
+        out = C.c_int64()
+        if p.dtype == np.float32:
+            p = np.ascontiguousarray(p)
+            self.check(self.lib.lsm_cloud_upload(self.handle, _ptr(p, C.c_float), len(p),
+                                                 C.byref(out)), "lsm_cloud_upload")
+        else:
+            p = np.ascontiguousarray(p, dtype=np.float64)
+            self.check(self.lib.lsm_cloud_upload_f64(self.handle, _ptr(p, C.c_double), len(p),
+                                                     C.byref(out)), "lsm_cloud_upload_f64")
+        return out.value
+
+    def release(self, cloud: int):
+        self.check(self.lib.lsm_cloud_release(self.handle, int(cloud)), "lsm_cloud_release")
+
+    def info(self, cloud: int):
+        nr, npr, hn = C.c_int64(), C.c_int64(), C.c_int32()
+        self.check(self.lib.lsm_cloud_info(self.handle, int(cloud), C.byref(nr), C.byref(npr),
+                                           C.byref(hn)), "lsm_cloud_info")
+        return nr.value, npr.value, bool(hn.value)
+
+    def preprocess(self, clouds, params: PrepParams) -> np.ndarray:
+        ids = np.ascontiguousarray(np.atleast_1d(np.asarray(clouds, dtype=np.int64)))
+        n_out = np.zeros(len(ids), dtype=np.int64)
+        self.check(self.lib.lsm_preprocess_batch(self.handle, len(ids), _ptr(ids, C.c_int64),
+                                                 C.byref(params), _ptr(n_out, C.c_int64)),
+                   "lsm_preprocess_batch")
+        return n_out
+
+    def download(self, cloud: int, normals: bool = False):
+        _, n, hn = self.info(cloud)
+        xyz = np.empty((n, 3), dtype=np.float64)
+        nrm = np.empty((n, 3), dtype=np.float64) if normals else None
+        self.check(self.lib.lsm_cloud_download(
+            self.handle, int(cloud), _ptr(xyz, C.c_double),
+            _ptr(nrm, C.c_double) if nrm is not None else None, n), "lsm_cloud_download")
+        return (xyz, nrm) if normals else xyz
+
+    def voxel_keys(self, cloud: int) -> np.ndarray:
+        _, n, _ = self.info(cloud)
+        k = np.empty((n, 3), dtype=np.int32)
+        self.check(self.lib.lsm_cloud_voxel_keys(self.handle, int(cloud), _ptr(k, C.c_int32), n),
+                   "lsm_cloud_voxel_keys")
+        return k
+
+    # -- registration ------------------------------------------------------------------------
+    def icp_batch(self, src, tgt, init, params: IcpParams):
+        s = np.ascontiguousarray(np.atleast_1d(np.asarray(src, dtype=np.int64)))
+        t = np.ascontiguousarray(np.atleast_1d(np.asarray(tgt, dtype=np.int64)))
+        if len(s) != len(t):
+            raise ValueError("src and tgt must have the same length")
+        n = len(s)
+        ip = None
+        if init is not None:
+            ini = np.ascontiguousarray(np.asarray(init, dtype=np.float64).reshape(n, 16))
+            ip = _ptr(ini, C.c_double)
+        res = (IcpResult * max(n, 1))()
+        self.check(self.lib.lsm_icp_batch(self.handle, n, _ptr(s, C.c_int64), _ptr(t, C.c_int64),
+                                          ip, C.byref(params), res), "registration_icp")
+        out = []
+        for k in range(n):
+            r = res[k]
+            out.append(dict(transformation=np.array(r.transformation[:]).reshape(4, 4),
+                            fitness=r.fitness, inlier_rmse=r.inlier_rmse,
+                            n_corr=int(r.correspondences), iterations=int(r.iterations),
+                            status=int(r.status)))
+        return out
+
+    def last_correspondences(self) -> np.ndarray:
+        n = C.c_int64()
+        self.check(self.lib.lsm_icp_last_correspondences(self.handle, None, 0, C.byref(n)),
+                   "lsm_icp_last_correspondences")
+        out = np.empty((n.value, 2), dtype=np.int64)
+        self.check(self.lib.lsm_icp_last_correspondences(self.handle, _ptr(out, C.c_int64),
+                                                         n.value, C.byref(n)),
+                   "lsm_icp_last_correspondences")
+        return out
+
+    # -- loop closure ------------------------------------------------------------------------
+    def loop_candidates(self, positions, distance_backwards, radius_threshold):
+        P = np.ascontiguousarray(np.asarray(positions, dtype=np.float64).reshape(-1, 3))
+        m = len(P)
+        cand = np.empty(max(m, 1), dtype=np.int64)
+        idx, nc = C.c_int64(), C.c_int64()
+        self.check(self.lib.lsm_loop_candidates(self.handle, _ptr(P, C.c_double), m,
+                                                float(distance_backwards),
+                                                float(radius_threshold), C.byref(idx),
+                                                _ptr(cand, C.c_int64), len(cand), C.byref(nc)),
+                   "lsm_loop_candidates")
+        return (None if idx.value < 0 else int(idx.value)), cand[:nc.value].copy()
+
+    def loop_partners(self, positions, candidates):
+        P = np.ascontiguousarray(np.asarray(positions, dtype=np.float64).reshape(-1, 3))
+        c = np.ascontiguousarray(np.asarray(candidates, dtype=np.int64))
+        part = np.empty(max(len(c), 1), dtype=np.int64)
+        self.check(self.lib.lsm_loop_triplet_partners(self.handle, _ptr(P, C.c_double), len(P),
+                                                      _ptr(c, C.c_int64), len(c),
+                                                      _ptr(part, C.c_int64)),
+                   "lsm_loop_triplet_partners")
+        return part[:len(c)].copy()
+
+    # -- instrumentation ---------------------------------------------------------------------
+    def set_timing(self, on: bool):
+        self.check(self.lib.lsm_set_timing(self.handle, 1 if on else 0), "lsm_set_timing")
+
+    def kernel_stats(self, name: str):
+        n, ms, b = C.c_int64(), C.c_double(), C.c_double()
+        self.check(self.lib.lsm_kernel_stats(self.handle, name.encode(), C.byref(n), C.byref(ms),
+                                             C.byref(b)), "lsm_kernel_stats")
+        return dict(launches=n.value, ms=ms.value, algo_bytes=b.value)
+
+    def reset_stats(self):
+        self.check(self.lib.lsm_reset_stats(self.handle), "lsm_reset_stats")
+
+
+_devices: dict = {}
+_dev_lock = threading.Lock()
+
+
+def device(index: int | None = None) -> Device:
+    """Per-process default context (LOCAL_RANK or 0 unless given)."""
+    if index is None:
+        index = int(os.environ.get("LSM_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    with _dev_lock:
+        d = _devices.get(index)
+        if d is None:
+            d = Device(index)
+            _devices[index] = d
+        return d
+
+
+def prep_params(min_radius=0.5, max_radius=35.0, min_height=-1.0, max_height=50.0,
+                voxel_size=None, normal_radius=0.3, max_nn=300, want_normals=True,
+                grid_cell=0.0) -> PrepParams:
+    return PrepParams(float(min_radius), float(max_radius), float(min_height), float(max_height),
+                      float(voxel_size) if voxel_size is not None else 0.0, float(normal_radius),
+                      int(max_nn), 1 if want_normals else 0, float(grid_cell))
+
+
+def icp_params(max_correspondence_distance=10.0, method="p2plane", max_iteration=30,
+               relative_fitness=1e-6, relative_rmse=1e-6) -> IcpParams:
+    m = {"p2p": LSM_P2P, "pointpoint": LSM_P2P, "p2plane": LSM_P2PLANE,
+         "pointplane": LSM_P2PLANE}.get(method, method)
+    if m not in (LSM_P2P, LSM_P2PLANE):
+        raise ValueError(f"unknown estimation method {method!r}")
+    return IcpParams(float(max_correspondence_distance), int(m), int(max_iteration),
+                     float(relative_fitness), float(relative_rmse))

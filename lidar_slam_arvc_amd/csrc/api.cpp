@@ -1,0 +1,447 @@
+// api.cpp -- the extern "C" boundary of liblidarsm (include/lidarsm.h).
+//
+// Thin validation + bookkeeping layer: argument errors are reported the way Open3D reports them
+// (LogError -> RuntimeError in the reference's Python), device work lives in prep.hip / icp.hip
+// / loop.hip. There is no CPU fallback: without a gfx950 device lsm_init fails.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lsm_ctx.h"
+
+static const char *kVersion = "liblidarsm 0.1 (gfx950)";
+
+// ------------------------------------------------------------------------------------------
+// lsm_ctx helpers
+// ------------------------------------------------------------------------------------------
+void *lsm_ctx::buf(const std::string &name, size_t bytes) {
+    DevBuf &b = scratch[name];
+    if (bytes == 0) bytes = 16;
+    if (b.bytes < bytes) {
+        if (b.p) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipFree(b.p);
+            b.p = nullptr;
+            b.bytes = 0;
+        }
+        size_t want = bytes + bytes / 4;
+        if (hipMalloc(&b.p, want) != hipSuccess) {
+            b.p = nullptr;
+            return nullptr;
+        }
+        b.bytes = want;
+    }
+    return b.p;
+}
+
+void *lsm_ctx::host_pinned(size_t bytes) {
+    if (pinned_bytes < bytes) {
+        if (pinned) (void)hipHostFree(pinned);
+        pinned = nullptr;
+        pinned_bytes = 0;
+        size_t want = bytes < 4096 ? 4096 : bytes * 2;
+        if (hipHostMalloc(&pinned, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+        pinned_bytes = want;
+    }
+    return pinned;
+}
+
+hipEvent_t lsm_ctx::get_event() {
+    if (!event_pool.empty()) {
+        hipEvent_t e = event_pool.back();
+        event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+void lsm_ctx::tic(const char *name, hipEvent_t *a) {
+    (void)name;
+    *a = nullptr;
+    if (!timing) return;
+    *a = get_event();
+    (void)hipEventRecord(*a, stream);
+}
+
+void lsm_ctx::toc(const char *name, hipEvent_t a) {
+    if (!timing || !a) return;
+    hipEvent_t b = get_event();
+    (void)hipEventRecord(b, stream);
+    pending.push_back({name, a, b});
+}
+
+void lsm_ctx::collect_timings() {
+    for (auto &pe : pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+            KStat &s = stats[pe.name];
+            s.launches += 1;
+            s.ms += ms;
+        }
+        event_pool.push_back(pe.a);
+        event_pool.push_back(pe.b);
+    }
+    pending.clear();
+}
+
+static Cloud *find_cloud(lsm_ctx *ctx, lsm_cloud id) {
+    auto it = ctx->clouds.find(id);
+    return it == ctx->clouds.end() ? nullptr : it->second;
+}
+
+static void free_cloud(Cloud *c) {
+    (void)hipFree(c->d_raw);
+    (void)hipFree(c->d_xyz);
+    (void)hipFree(c->d_nrm);
+    (void)hipFree(c->d_perm);
+    (void)hipFree(c->d_cell);
+    (void)hipFree(c->d_vox);
+    (void)hipFree(c->d_vkeys);
+    delete c;
+}
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+const char *lsm_version(void) { return kVersion; }
+
+void lsm_default_prep_params(lsm_prep_params *p) {
+    if (!p) return;
+    p->min_radius = 0.5;      // icp_parameters.yaml filter_by_radius.min_radius
+    p->max_radius = 35.0;     // icp_parameters.yaml filter_by_radius.max_radius
+    p->min_height = -1.0;     // icp_parameters.yaml filter_by_height.min_height
+    p->max_height = 50.0;     // icp_parameters.yaml filter_by_height.max_height
+    p->voxel_size = 0.0;      // down_sample.voxel_size: null
+    p->normal_radius = 0.3;   // keyframe.py:33
+    p->max_nn = 300;          // normals.maximum_neighbors
+    p->want_normals = 1;      // method 'icppointplane' (keyframemanager.py:9)
+    p->grid_cell = 0.0;
+}
+
+void lsm_default_icp_params(lsm_icp_params *p) {
+    if (!p) return;
+    p->max_correspondence_distance = 10.0;  // icp.distance_threshold
+    p->method = LSM_P2PLANE;
+    p->max_iteration = 30;                  // Open3D ICPConvergenceCriteria defaults
+    p->relative_fitness = 1e-6;
+    p->relative_rmse = 1e-6;
+}
+
+int lsm_init(int device, lsm_ctx **out) {
+    if (!out) return LSM_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return LSM_ENODEV;
+    if (device < 0 || device >= ndev) return LSM_EINVAL;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return LSM_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return LSM_ENODEV;
+    if (hipSetDevice(device) != hipSuccess) return LSM_EHIP;
+    lsm_ctx *ctx = new lsm_ctx();
+    ctx->device = device;
+    ctx->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return LSM_EHIP;
+    }
+    *out = ctx;
+    return LSM_OK;
+}
+
+int lsm_free(lsm_ctx *ctx) {
+    if (!ctx) return LSM_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto &kv : ctx->clouds) free_cloud(kv.second);
+    for (auto &kv : ctx->scratch) (void)hipFree(kv.second.p);
+    for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    for (auto &pe : ctx->pending) {
+        (void)hipEventDestroy(pe.a);
+        (void)hipEventDestroy(pe.b);
+    }
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return LSM_OK;
+}
+
+const char *lsm_last_error(lsm_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+static int upload_common(lsm_ctx *ctx, const void *xyz, int64_t n, bool f64, lsm_cloud *out) {
+    if (!ctx || !out || n < 0 || (n > 0 && !xyz)) return LSM_EINVAL;
+    if (n >= (int64_t(1) << 31)) {
+        ctx->set_error("cloud too large (>= 2^31 points)");
+        return LSM_EINVAL;
+    }
+    (void)hipSetDevice(ctx->device);
+    Cloud *c = new Cloud();
+    c->n_raw = n;
+    size_t bytes = size_t(n > 0 ? n : 1) * 3 * sizeof(float);
+    if (hipMalloc(&c->d_raw, bytes) != hipSuccess) {
+        delete c;
+        ctx->set_error("hipMalloc failed for raw cloud");
+        return LSM_ENOMEM;
+    }
+    if (n > 0) {
+        if (!f64) {
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_raw, xyz, size_t(n) * 12, hipMemcpyHostToDevice,
+                                            ctx->stream));
+        } else {
+            std::vector<float> tmp(size_t(n) * 3);
+            const double *d = static_cast<const double *>(xyz);
+            for (size_t i = 0; i < tmp.size(); ++i) tmp[i] = float(d[i]);
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_raw, tmp.data(), tmp.size() * 4,
+                                            hipMemcpyHostToDevice, ctx->stream));
+            LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        }
+    }
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int64_t id = ctx->next_id++;
+    ctx->clouds[id] = c;
+    *out = id;
+    return LSM_OK;
+}
+
+int lsm_cloud_upload(lsm_ctx *ctx, const float *xyz, int64_t n, lsm_cloud *out) {
+    return upload_common(ctx, xyz, n, false, out);
+}
+
+int lsm_cloud_upload_f64(lsm_ctx *ctx, const double *xyz, int64_t n, lsm_cloud *out) {
+    return upload_common(ctx, xyz, n, true, out);
+}
+
+int lsm_cloud_release(lsm_ctx *ctx, lsm_cloud cloud) {
+    if (!ctx) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    free_cloud(c);
+    ctx->clouds.erase(cloud);
+    return LSM_OK;
+}
+
+int lsm_cloud_info(lsm_ctx *ctx, lsm_cloud cloud, int64_t *n_raw, int64_t *n_proc,
+                   int32_t *has_normals) {
+    if (!ctx) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (n_raw) *n_raw = c->n_raw;
+    if (n_proc) *n_proc = c->processed ? c->n : 0;
+    if (has_normals) *has_normals = c->has_normals ? 1 : 0;
+    return LSM_OK;
+}
+
+static int check_prep(lsm_ctx *ctx, const lsm_prep_params *p) {
+    if (!p) return LSM_EINVAL;
+    if (!(p->max_radius > 0) || !std::isfinite(p->max_radius) || !std::isfinite(p->min_height) ||
+        !std::isfinite(p->max_height)) {
+        ctx->set_error("filter bounds must be finite (max_radius > 0)");
+        return LSM_EINVAL;
+    }
+    if (p->want_normals && (!(p->normal_radius > 0) || p->max_nn < 0)) {
+        ctx->set_error("Invalid KDTreeSearchParamHybrid (radius <= 0 or max_nn < 0)");
+        return LSM_EINVAL;
+    }
+    return LSM_OK;
+}
+
+int lsm_preprocess_batch(lsm_ctx *ctx, int64_t n, const lsm_cloud *clouds,
+                         const lsm_prep_params *p, int64_t *n_out) {
+    if (!ctx || n < 0 || (n > 0 && !clouds)) return LSM_EINVAL;
+    int rc = check_prep(ctx, p);
+    if (rc) return rc;
+    std::vector<Cloud *> cs;
+    cs.reserve(size_t(n));
+    for (int64_t i = 0; i < n; ++i) {
+        Cloud *c = find_cloud(ctx, clouds[i]);
+        if (!c) {
+            ctx->set_error("unknown cloud handle");
+            return LSM_EINVAL;
+        }
+        for (Cloud *o : cs)
+            if (o == c) {
+                ctx->set_error("duplicate cloud in preprocess batch");
+                return LSM_EINVAL;
+            }
+        cs.push_back(c);
+    }
+    if (n == 0) return LSM_OK;
+    (void)hipSetDevice(ctx->device);
+    return lsm_prep_batch(ctx, cs, *p, n_out);
+}
+
+int lsm_preprocess(lsm_ctx *ctx, lsm_cloud cloud, const lsm_prep_params *p, int64_t *n_out) {
+    return lsm_preprocess_batch(ctx, 1, &cloud, p, n_out);
+}
+
+int lsm_cloud_download(lsm_ctx *ctx, lsm_cloud cloud, double *xyz, double *normals,
+                       int64_t cap) {
+    if (!ctx) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!c->processed) {
+        ctx->set_error("cloud has not been pre-processed");
+        return LSM_ESTATE;
+    }
+    if (cap < c->n) {
+        ctx->set_error("output capacity smaller than the processed cloud");
+        return LSM_EINVAL;
+    }
+    if (normals && !c->has_normals) {
+        ctx->set_error("cloud has no normals");
+        return LSM_ESTATE;
+    }
+    (void)hipSetDevice(ctx->device);
+    return lsm_download_run(ctx, c, xyz, normals, cap);
+}
+
+int lsm_cloud_voxel_keys(lsm_ctx *ctx, lsm_cloud cloud, int32_t *keys, int64_t cap) {
+    if (!ctx || !keys) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!c->processed || !c->voxelized) {
+        ctx->set_error("cloud is not voxel-down-sampled");
+        return LSM_ESTATE;
+    }
+    if (cap < c->n) return LSM_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    if (c->n > 0) {
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(keys, c->d_vkeys, size_t(c->n) * 12,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+    }
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return LSM_OK;
+}
+
+static int check_icp(lsm_ctx *ctx, const lsm_icp_params *p) {
+    if (!p) return LSM_EINVAL;
+    if (!(p->max_correspondence_distance > 0.0)) {
+        ctx->set_error("Invalid max_correspondence_distance.");
+        return LSM_EINVAL;
+    }
+    if (p->method != LSM_P2P && p->method != LSM_P2PLANE) {
+        ctx->set_error("unknown transformation estimation method");
+        return LSM_EINVAL;
+    }
+    if (p->max_iteration < 0) {
+        ctx->set_error("max_iteration must be >= 0");
+        return LSM_EINVAL;
+    }
+    return LSM_OK;
+}
+
+int lsm_icp_batch(lsm_ctx *ctx, int64_t npairs, const lsm_cloud *src, const lsm_cloud *tgt,
+                  const double *init, const lsm_icp_params *p, lsm_icp_result *out) {
+    if (!ctx || npairs < 0 || (npairs > 0 && (!src || !tgt || !out))) return LSM_EINVAL;
+    int rc = check_icp(ctx, p);
+    if (rc) return rc;
+    std::vector<Cloud *> s(static_cast<size_t>(npairs)), t(static_cast<size_t>(npairs));
+    for (int64_t i = 0; i < npairs; ++i) {
+        s[i] = find_cloud(ctx, src[i]);
+        t[i] = find_cloud(ctx, tgt[i]);
+        if (!s[i] || !t[i]) {
+            ctx->set_error("unknown cloud handle");
+            return LSM_EINVAL;
+        }
+        if (!s[i]->processed || !t[i]->processed) {
+            ctx->set_error("registration needs pre-processed clouds (KeyFrame.pre_process)");
+            return LSM_ESTATE;
+        }
+        if (p->method == LSM_P2PLANE && !t[i]->has_normals) {
+            ctx->set_error("TransformationEstimationPointToPlane and "
+                           "TransformationEstimationColoredICP require pre-computed normal "
+                           "vectors for target PointCloud.");
+            return LSM_ESTATE;
+        }
+    }
+    if (npairs == 0) return LSM_OK;
+    (void)hipSetDevice(ctx->device);
+    return lsm_icp_run(ctx, npairs, s.data(), t.data(), init, *p, out);
+}
+
+int lsm_icp(lsm_ctx *ctx, lsm_cloud src, lsm_cloud tgt, const double init[16],
+            const lsm_icp_params *p, lsm_icp_result *out) {
+    return lsm_icp_batch(ctx, 1, &src, &tgt, init, p, out);
+}
+
+int lsm_icp_last_correspondences(lsm_ctx *ctx, int64_t *pairs, int64_t cap, int64_t *n) {
+    if (!ctx || !n) return LSM_EINVAL;
+    int64_t m = int64_t(ctx->last_corr.size() / 2);
+    *n = m;
+    if (pairs) {
+        if (cap < m) return LSM_EINVAL;
+        std::memcpy(pairs, ctx->last_corr.data(), ctx->last_corr.size() * sizeof(int64_t));
+    }
+    return LSM_OK;
+}
+
+int lsm_loop_candidates(lsm_ctx *ctx, const double *positions, int64_t m,
+                        double distance_backwards, double radius_threshold,
+                        int64_t *index_backwards, int64_t *candidates, int64_t cap,
+                        int64_t *n_candidates) {
+    if (!ctx || m < 0 || (m > 0 && !positions) || !index_backwards || !n_candidates)
+        return LSM_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    return lsm_loop_candidates_run(ctx, positions, m, distance_backwards, radius_threshold,
+                                   index_backwards, candidates, cap, n_candidates);
+}
+
+int lsm_loop_triplet_partners(lsm_ctx *ctx, const double *positions, int64_t m,
+                              const int64_t *candidates, int64_t n_candidates, int64_t *partner) {
+    if (!ctx || m < 0 || n_candidates < 0 || (n_candidates > 0 && (!candidates || !partner)))
+        return LSM_EINVAL;
+    for (int64_t k = 0; k < n_candidates; ++k)
+        if (candidates[k] < 0 || candidates[k] >= m) {
+            ctx->set_error("candidate index out of range");
+            return LSM_EINVAL;
+        }
+    if (n_candidates == 0) return LSM_OK;
+    (void)hipSetDevice(ctx->device);
+    return lsm_loop_partners_run(ctx, positions, m, candidates, n_candidates, partner);
+}
+
+int lsm_set_timing(lsm_ctx *ctx, int32_t enable) {
+    if (!ctx) return LSM_EINVAL;
+    ctx->timing = enable != 0;
+    return LSM_OK;
+}
+
+int lsm_kernel_stats(lsm_ctx *ctx, const char *kernel, int64_t *launches, double *total_ms,
+                     double *algo_bytes) {
+    if (!ctx || !kernel) return LSM_EINVAL;
+    auto it = ctx->stats.find(kernel);
+    KStat s;
+    if (it != ctx->stats.end()) s = it->second;
+    if (launches) *launches = s.launches;
+    if (total_ms) *total_ms = s.ms;
+    if (algo_bytes) *algo_bytes = s.algo_bytes;
+    return LSM_OK;
+}
+
+int lsm_reset_stats(lsm_ctx *ctx) {
+    if (!ctx) return LSM_EINVAL;
+    ctx->stats.clear();
+    return LSM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,813 @@
+// icp.hip -- registration_icp on the device (keyframe.py:231-260 -> [O3D] RegistrationICP),
+// batched over independent keyframe pairs.
+//
+// One correspondence pass (GetRegistrationResultAndCorrespondences) + one update
+// (TransformationEstimationPointToPlane / PointToPoint::ComputeTransformation) per launch group:
+//
+//   nn_kernel          one lane per source point: transform by the pair's T (f64), exact 1-NN in
+//                      the target's cell grid (own cell, then the 26 neighbours pruned by their
+//                      lower-bound distance). A query whose nearest point is provably inside the
+//                      3x3x3 block is resolved; the rest (a few %) go to a queue.
+//   nn_fallback        one wave per queued query: expanding boxes, the wave strides over each
+//                      cell row, (d2, index) wave-min -> exact nearest within max_corr.
+//   accumulate         one lane per source point: f64 residual / Jacobian of the correspondence,
+//                      fixed-tree wave + LDS reduction into per-block partials (deterministic).
+//   solve              one wave per pair: ordered sum of the pair's partials, fitness / rmse,
+//                      Open3D's convergence rule, Eigen-style LDLT (P2Plane) or Horn/Umeyama
+//                      (P2P), T <- dT * T.
+//
+// Correspondences use d^2 < max_corr^2 (SearchHybrid + lower_bound); fitness = |C| / N_src,
+// inlier_rmse = sqrt(sum d^2 / |C|) (0, 0 when C is empty); empty C -> identity update.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <unordered_map>
+#include <vector>
+
+#include "lsm_ctx.h"
+
+namespace {
+
+constexpr int NN_THREADS = 256;
+constexpr int NXCD = 8;
+
+struct NNParams {
+    float maxc2;       // max_correspondence_distance^2 (f32, correspondence test)
+    float maxc;        // max_correspondence_distance
+    int method;
+    int max_iter;
+    double rel_fit, rel_rmse;
+};
+
+struct FallbackItem {
+    int32_t pair;
+    int32_t i;        // source point (sorted order)
+    int32_t best;     // best target index found by nn_kernel (-1 none)
+    float best_d2;
+};
+
+__device__ __forceinline__ bool better(float d2, int idx, float bd2, int bidx) {
+    return d2 < bd2 || (d2 == bd2 && idx < bidx);
+}
+
+__device__ __forceinline__ void transform_point(const double *T, float4 p, double &x, double &y,
+                                                double &z) {
+    const double px = p.x, py = p.y, pz = p.z;
+    x = T[0] * px + T[1] * py + T[2] * pz + T[3];
+    y = T[4] * px + T[5] * py + T[6] * pz + T[7];
+    z = T[8] * px + T[9] * py + T[10] * pz + T[11];
+}
+
+__device__ __forceinline__ void scan_run(const float4 *__restrict__ xyz, uint32_t a, uint32_t b,
+                                         float qx, float qy, float qz, float &bd2, int &bidx) {
+    for (uint32_t k = a; k < b; ++k) {
+        const float4 t = xyz[k];
+        const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
+        const float d2 = dx * dx + dy * dy + dz * dz;
+        if (better(d2, int(k), bd2, bidx)) {
+            bd2 = d2;
+            bidx = int(k);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// correspondence search (the hot kernel)
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(NN_THREADS)
+nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
+          const CloudDev *__restrict__ cds, NNParams prm, int32_t *__restrict__ corr,
+          float *__restrict__ corr_d2, FallbackItem *__restrict__ queue,
+          uint32_t *__restrict__ queue_n, uint32_t queue_cap) {
+    const BlockTask task = tasks[blockIdx.x];
+    if (task.pair < 0) return;
+    const PairState &P = st[task.pair];
+    if (!P.active) return;
+    const CloudDev S = cds[P.src];
+    const CloudDev G = cds[P.tgt];
+    const int i = task.start + threadIdx.x;
+    const bool live = i < S.n;
+    int result = -1;
+    float bd2 = INFINITY;
+    int bidx = -1;
+    bool pending = false;
+    if (live) {
+        double qx64, qy64, qz64;
+        transform_point(P.T, S.xyz[i], qx64, qy64, qz64);
+        const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
+        const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
+                    fz = (qz - G.oz) * G.inv_cell;
+        const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
+        const bool inside = G.n > 0 && cx >= 0 && cx < G.nx && cy >= 0 && cy < G.ny && cz >= 0 &&
+                            cz < G.nz;
+        if (!inside) {
+            pending = G.n > 0;   // outside the target's box: let the fallback decide
+        } else {
+            const float ax = fx - cx, ay = fy - cy, az = fz - cz;
+            const float c2s = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
+            // squared distance (in cells^2) from q to the neighbour slab on each side
+            const float lx = ax * ax, hx = (1.f - ax) * (1.f - ax);
+            const float ly = ay * ay, hy = (1.f - ay) * (1.f - ay);
+            const float lz = az * az, hz = (1.f - az) * (1.f - az);
+            const uint32_t *cs = G.cell_start;
+            // own cell first
+            {
+                const int lin = (cz * G.ny + cy) * G.nx + cx;
+                scan_run(G.xyz, cs[lin], cs[lin + 1], qx, qy, qz, bd2, bidx);
+            }
+#pragma unroll 1
+            for (int dz = -1; dz <= 1; ++dz) {
+                const int z = cz + dz;
+                if (z < 0 || z >= G.nz) continue;
+                const float wz = (dz < 0 ? lz : (dz > 0 ? hz : 0.f)) * c2s;
+                if (wz >= bd2) continue;
+#pragma unroll 1
+                for (int dy = -1; dy <= 1; ++dy) {
+                    const int y = cy + dy;
+                    if (y < 0 || y >= G.ny) continue;
+                    const float wyz = wz + (dy < 0 ? ly : (dy > 0 ? hy : 0.f)) * c2s;
+                    if (wyz >= bd2) continue;
+                    const int row = (z * G.ny + y) * G.nx;
+#pragma unroll 1
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        if ((dx | dy | dz) == 0) continue;
+                        const int x = cx + dx;
+                        if (x < 0 || x >= G.nx) continue;
+                        const float w = wyz + (dx < 0 ? lx : (dx > 0 ? hx : 0.f)) * c2s;
+                        if (w >= bd2) continue;
+                        scan_run(G.xyz, cs[row + x], cs[row + x + 1], qx, qy, qz, bd2, bidx);
+                    }
+                }
+            }
+            // every point outside the 3x3x3 block is at least `bound` away (in cells); sides
+            // clipped by the grid hold no points.
+            float bx = fminf(cx >= 2 ? ax + 1.f : INFINITY, cx + 2 < G.nx ? 2.f - ax : INFINITY);
+            float by = fminf(cy >= 2 ? ay + 1.f : INFINITY, cy + 2 < G.ny ? 2.f - ay : INFINITY);
+            float bz = fminf(cz >= 2 ? az + 1.f : INFINITY, cz + 2 < G.nz ? 2.f - az : INFINITY);
+            const float bound = fminf(bx, fminf(by, bz)) * G.cell;
+            const float bound2 = bound * bound * 0.99999f;
+            if (bd2 <= bound2 || bound >= prm.maxc) {
+                result = (bidx >= 0 && bd2 < prm.maxc2) ? bidx : -1;
+            } else {
+                pending = true;
+            }
+        }
+    }
+    // wave-aggregated queue append
+    const uint64_t m = __ballot(pending);
+    if (m) {
+        const int lane = threadIdx.x & 63;
+        uint32_t base = 0;
+        if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(queue_n, (uint32_t)__popcll(m));
+        base = __shfl(base, __ffsll((unsigned long long)m) - 1, LSM_WAVE);
+        if (pending) {
+            const uint32_t slot = base + __popcll(m & ((uint64_t(1) << lane) - 1));
+            if (slot < queue_cap) queue[slot] = {task.pair, i, bidx, bd2};
+        }
+    }
+    if (live) {
+        const int64_t g = P.src_off + i;
+        corr[g] = pending ? -2 : result;
+        corr_d2[g] = bd2;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// exact fallback: one wave per unresolved query, expanding boxes (shells)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_argmin(float &d2, int &idx) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float od = __shfl_xor(d2, off, LSM_WAVE);
+        const int oi = __shfl_xor(idx, off, LSM_WAVE);
+        if (better(od, oi, d2, idx)) {
+            d2 = od;
+            idx = oi;
+        }
+    }
+}
+
+__device__ __forceinline__ float gap2(float q, float lo, float hi) {
+    const float d = q < lo ? lo - q : (q > hi ? q - hi : 0.f);
+    return d * d;
+}
+
+__global__ void __launch_bounds__(LSM_WAVE)
+nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
+            const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
+            uint32_t queue_cap, int32_t *__restrict__ corr, float *__restrict__ corr_d2) {
+    const int lane = threadIdx.x;
+    const uint32_t total = min(*queue_n, queue_cap);
+    for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
+        const FallbackItem q = queue[it];
+        const PairState &P = st[q.pair];
+        const CloudDev S = cds[P.src];
+        const CloudDev G = cds[P.tgt];
+        double qx64, qy64, qz64;
+        transform_point(P.T, S.xyz[q.i], qx64, qy64, qz64);
+        const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
+        float bd2 = q.best_d2;
+        int bidx = q.best;
+        // previous box (cell ranges already fully examined); start with the 3x3x3 block or none
+        const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
+                    fz = (qz - G.oz) * G.inv_cell;
+        const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
+        const bool inside =
+            cx >= 0 && cx < G.nx && cy >= 0 && cy < G.ny && cz >= 0 && cz < G.nz;
+        int pxl = 1, pxh = 0, pyl = 1, pyh = 0, pzl = 1, pzh = 0;  // empty
+        if (inside) {
+            pxl = max(cx - 1, 0);
+            pxh = min(cx + 1, G.nx - 1);
+            pyl = max(cy - 1, 0);
+            pyh = min(cy + 1, G.ny - 1);
+            pzl = max(cz - 1, 0);
+            pzh = min(cz + 1, G.nz - 1);
+        }
+        float s = 4.f * G.cell;
+        for (int level = 0; level < 16; ++level) {
+            if (s > prm.maxc) s = prm.maxc;
+            const float h = s * G.inv_cell;
+            int xl = (int)floorf(fx - h - 1e-3f), xh = (int)floorf(fx + h + 1e-3f);
+            int yl = (int)floorf(fy - h - 1e-3f), yh = (int)floorf(fy + h + 1e-3f);
+            int zl = (int)floorf(fz - h - 1e-3f), zh = (int)floorf(fz + h + 1e-3f);
+            xl = max(xl, 0);
+            yl = max(yl, 0);
+            zl = max(zl, 0);
+            xh = min(xh, G.nx - 1);
+            yh = min(yh, G.ny - 1);
+            zh = min(zh, G.nz - 1);
+            for (int z = zl; z <= zh; ++z) {
+                const float wz = gap2(qz, G.oz + z * G.cell, G.oz + (z + 1) * G.cell);
+                if (wz >= bd2) continue;
+                for (int y = yl; y <= yh; ++y) {
+                    const float wyz = wz + gap2(qy, G.oy + y * G.cell, G.oy + (y + 1) * G.cell);
+                    if (wyz >= bd2) continue;
+                    const int row = (z * G.ny + y) * G.nx;
+                    const bool inner = (y >= pyl && y <= pyh && z >= pzl && z <= pzh);
+                    // up to two x-runs: [xl, pxl-1] and [pxh+1, xh] when the row crosses the
+                    // previous box, else [xl, xh]
+                    int ra0 = xl, rb0 = xh, ra1 = 1, rb1 = 0;
+                    if (inner && pxl <= pxh) {
+                        rb0 = min(xh, pxl - 1);
+                        ra1 = max(xl, pxh + 1);
+                        rb1 = xh;
+                    }
+                    for (int r = 0; r < 2; ++r) {
+                        const int a = r ? ra1 : ra0, b = r ? rb1 : rb0;
+                        if (a > b) continue;
+                        const float wx = gap2(qx, G.ox + a * G.cell, G.ox + (b + 1) * G.cell);
+                        if (wyz + wx >= bd2) continue;
+                        const uint32_t pa = G.cell_start[row + a], pb = G.cell_start[row + b + 1];
+                        for (uint32_t k = pa + lane; k < pb; k += LSM_WAVE) {
+                            const float4 t = G.xyz[k];
+                            const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
+                            const float d2 = dx * dx + dy * dy + dz * dz;
+                            if (better(d2, int(k), bd2, bidx)) {
+                                bd2 = d2;
+                                bidx = int(k);
+                            }
+                        }
+                    }
+                }
+                // keep the wave's best in sync so pruning tightens
+                wave_argmin(bd2, bidx);
+            }
+            wave_argmin(bd2, bidx);
+            if (bd2 <= s * s * 0.99999f || s >= prm.maxc) break;
+            pxl = xl;
+            pxh = xh;
+            pyl = yl;
+            pyh = yh;
+            pzl = zl;
+            pzh = zh;
+            s *= 4.f;
+        }
+        if (lane == 0) {
+            const int64_t g = P.src_off + q.i;
+            corr[g] = (bidx >= 0 && bd2 < prm.maxc2) ? bidx : -1;
+            corr_d2[g] = bd2;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// residual / Jacobian accumulation (deterministic block partials)
+// ------------------------------------------------------------------------------------------
+template <int METHOD>
+__global__ void __launch_bounds__(NN_THREADS)
+accumulate_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
+                  const CloudDev *__restrict__ cds, const int32_t *__restrict__ corr,
+                  double *__restrict__ partials) {
+    const BlockTask task = tasks[blockIdx.x];
+    if (task.pair < 0) return;
+    const PairState &P = st[task.pair];
+    if (!P.active) return;
+    const CloudDev S = cds[P.src];
+    const CloudDev G = cds[P.tgt];
+    const int i = task.start + threadIdx.x;
+    double acc[30];
+#pragma unroll
+    for (int k = 0; k < 30; ++k) acc[k] = 0.0;
+    if (i < S.n) {
+        const int idx = corr[P.src_off + i];
+        if (idx >= 0) {
+            double x, y, z;
+            transform_point(P.T, S.xyz[i], x, y, z);
+            const float4 t = G.xyz[idx];
+            const double tx = t.x, ty = t.y, tz = t.z;
+            const double ex = x - tx, ey = y - ty, ez = z - tz;
+            acc[28] = (ex * ex + ey * ey) + ez * ez;
+            acc[29] = 1.0;
+            if (METHOD == LSM_P2PLANE) {
+                const float4 nf = G.nrm[idx];
+                const double nx = nf.x, ny = nf.y, nz = nf.z;
+                const double r = (ex * nx + ey * ny) + ez * nz;
+                const double J[6] = {y * nz - z * ny, z * nx - x * nz, x * ny - y * nx, nx, ny, nz};
+                int k = 0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a)
+#pragma unroll
+                    for (int b = a; b < 6; ++b) acc[k++] = J[a] * J[b];
+#pragma unroll
+                for (int a = 0; a < 6; ++a) acc[21 + a] = J[a] * r;
+                acc[27] = r * r;
+            } else {
+                acc[0] = x;
+                acc[1] = y;
+                acc[2] = z;
+                acc[3] = tx;
+                acc[4] = ty;
+                acc[5] = tz;
+                const double tv[3] = {tx, ty, tz}, sv[3] = {x, y, z};
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] = tv[a] * sv[b];
+            }
+        }
+    }
+    __shared__ double red[NN_THREADS / LSM_WAVE][30];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 30; ++k) {
+        const double v = lsm_wave_sum(acc[k]);
+        if (lane == 0) red[w][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 30) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < NN_THREADS / LSM_WAVE; ++q) s += red[q][threadIdx.x];
+        partials[size_t(task.slot) * LSM_ACC + threadIdx.x] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// solve: one wave per pair
+// ------------------------------------------------------------------------------------------
+// Eigen::LDLT (diagonal pivoting on the not-yet-updated diagonal, left-looking) + solve with the
+// pseudo-inverse of D (|D_i| <= DBL_MIN -> 0), as SolveLinearSystemPSD(JTJ, -JTr).
+__device__ void ldlt_solve6(double A[6][6], double b[6], double x[6]) {
+    int tr[6];
+    double diag_tmp[6];
+    for (int k = 0; k < 6; ++k) {
+        int j = k;
+        double best = fabs(A[k][k]);
+        for (int q = k + 1; q < 6; ++q)
+            if (fabs(A[q][q]) > best) {
+                best = fabs(A[q][q]);
+                j = q;
+            }
+        tr[k] = j;
+        if (j != k) {
+            for (int c = 0; c < 6; ++c) {
+                double t = A[k][c];
+                A[k][c] = A[j][c];
+                A[j][c] = t;
+            }
+            for (int r = 0; r < 6; ++r) {
+                double t = A[r][k];
+                A[r][k] = A[r][j];
+                A[r][j] = t;
+            }
+        }
+        if (k > 0) {
+            for (int c = 0; c < k; ++c) diag_tmp[c] = A[c][c] * A[k][c];
+            double s = 0.0;
+            for (int c = 0; c < k; ++c) s += A[k][c] * diag_tmp[c];
+            A[k][k] -= s;
+            for (int r = k + 1; r < 6; ++r) {
+                double t = 0.0;
+                for (int c = 0; c < k; ++c) t += A[r][c] * diag_tmp[c];
+                A[r][k] -= t;
+            }
+        }
+        const double akk = A[k][k];
+        if (k == 0 && akk == 0.0) {
+            for (int q = 0; q < 6; ++q) x[q] = 0.0;
+            return;
+        }
+        if (akk != 0.0)
+            for (int r = k + 1; r < 6; ++r) A[r][k] /= akk;
+    }
+    double y[6];
+    for (int q = 0; q < 6; ++q) y[q] = b[q];
+    for (int k = 0; k < 6; ++k) {
+        double t = y[k];
+        y[k] = y[tr[k]];
+        y[tr[k]] = t;
+    }
+    for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < r; ++c) y[r] -= A[r][c] * y[c];
+    for (int r = 0; r < 6; ++r) y[r] = fabs(A[r][r]) > 2.2250738585072014e-308 ? y[r] / A[r][r] : 0.0;
+    for (int r = 5; r >= 0; --r)
+        for (int c = r + 1; c < 6; ++c) y[r] -= A[c][r] * y[c];
+    for (int k = 5; k >= 0; --k) {
+        double t = y[k];
+        y[k] = y[tr[k]];
+        y[tr[k]] = t;
+    }
+    for (int q = 0; q < 6; ++q) x[q] = y[q];
+}
+
+// TransformVector6dToMatrix4d: R = Rz(x2) * Ry(x1) * Rx(x0), t = x3..5.
+__device__ void vec6_to_mat4(const double x[6], double D[16]) {
+    const double ca = cos(x[0]), sa = sin(x[0]), cb = cos(x[1]), sb = sin(x[1]), cg = cos(x[2]),
+                 sg = sin(x[2]);
+    D[0] = cg * cb;
+    D[1] = cg * sb * sa - sg * ca;
+    D[2] = cg * sb * ca + sg * sa;
+    D[4] = sg * cb;
+    D[5] = sg * sb * sa + cg * ca;
+    D[6] = sg * sb * ca - cg * sa;
+    D[8] = -sb;
+    D[9] = cb * sa;
+    D[10] = cb * ca;
+    D[3] = x[3];
+    D[7] = x[4];
+    D[11] = x[5];
+    D[12] = D[13] = D[14] = 0.0;
+    D[15] = 1.0;
+}
+
+// Largest-eigenvalue eigenvector of a symmetric 4x4 (cyclic Jacobi).
+__device__ void sym4_max_eigvec(double N[4][4], double v[4]) {
+    double V[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < 4; ++p)
+            for (int q = p + 1; q < 4; ++q) off += N[p][q] * N[p][q];
+        if (off < 1e-300) break;
+        for (int p = 0; p < 4; ++p)
+            for (int q = p + 1; q < 4; ++q) {
+                if (N[p][q] == 0.0) continue;
+                const double theta = (N[q][q] - N[p][p]) / (2.0 * N[p][q]);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 4; ++k) {
+                    const double a = N[k][p], b = N[k][q];
+                    N[k][p] = c * a - s * b;
+                    N[k][q] = s * a + c * b;
+                }
+                for (int k = 0; k < 4; ++k) {
+                    const double a = N[p][k], b = N[q][k];
+                    N[p][k] = c * a - s * b;
+                    N[q][k] = s * a + c * b;
+                }
+                for (int k = 0; k < 4; ++k) {
+                    const double a = V[k][p], b = V[k][q];
+                    V[k][p] = c * a - s * b;
+                    V[k][q] = s * a + c * b;
+                }
+            }
+    }
+    int best = 0;
+    for (int k = 1; k < 4; ++k)
+        if (N[k][k] > N[best][best]) best = k;
+    for (int k = 0; k < 4; ++k) v[k] = V[k][best];
+}
+
+// Umeyama (with_scaling = false): the rotation maximising tr(R^T Sigma), via Horn's quaternion.
+__device__ void umeyama_update(const double *tot, double D[16]) {
+    const double n = tot[29];
+    const double ms[3] = {tot[0] / n, tot[1] / n, tot[2] / n};
+    const double mt[3] = {tot[3] / n, tot[4] / n, tot[5] / n};
+    double H[3][3];  // H[a][b] = sum (s - ms)_a (t - mt)_b / n  (= Sigma^T)
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) H[a][b] = tot[6 + 3 * b + a] / n - mt[b] * ms[a];
+    const double Sxx = H[0][0], Sxy = H[0][1], Sxz = H[0][2], Syx = H[1][0], Syy = H[1][1],
+                 Syz = H[1][2], Szx = H[2][0], Szy = H[2][1], Szz = H[2][2];
+    double N[4][4] = {{Sxx + Syy + Szz, Syz - Szy, Szx - Sxz, Sxy - Syx},
+                      {Syz - Szy, Sxx - Syy - Szz, Sxy + Syx, Szx + Sxz},
+                      {Szx - Sxz, Sxy + Syx, -Sxx + Syy - Szz, Syz + Szy},
+                      {Sxy - Syx, Szx + Sxz, Syz + Szy, -Sxx - Syy + Szz}};
+    double q[4];
+    sym4_max_eigvec(N, q);
+    const double qn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const double w = q[0] / qn, x = q[1] / qn, y = q[2] / qn, z = q[3] / qn;
+    double R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w),     2 * (x * z + y * w),
+                   2 * (x * y + z * w),     1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                   2 * (x * z - y * w),     2 * (y * z + x * w),     1 - 2 * (x * x + y * y)};
+    for (int r = 0; r < 3; ++r) {
+        D[4 * r + 0] = R[3 * r + 0];
+        D[4 * r + 1] = R[3 * r + 1];
+        D[4 * r + 2] = R[3 * r + 2];
+        D[4 * r + 3] = mt[r] - (R[3 * r] * ms[0] + R[3 * r + 1] * ms[1] + R[3 * r + 2] * ms[2]);
+    }
+    D[12] = D[13] = D[14] = 0.0;
+    D[15] = 1.0;
+}
+
+__global__ void __launch_bounds__(LSM_WAVE)
+solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NNParams prm,
+             int pass, const double *__restrict__ pair_bytes, uint32_t *__restrict__ active_next,
+             double *__restrict__ bytes_next) {
+    PairState &P = st[blockIdx.x];
+    if (!P.active) return;
+    __shared__ double tot[32];
+    const int lane = threadIdx.x;
+    if (lane < 30) {
+        double s = 0.0;
+        for (int b = 0; b < P.nblk; ++b) s += partials[size_t(P.blk0 + b) * LSM_ACC + lane];
+        tot[lane] = s;
+    }
+    __syncthreads();
+    if (lane != 0) return;
+    const double cnt = tot[29];
+    const double nsrc = double(P.nsrc);
+    const double fitness = cnt > 0 ? cnt / nsrc : 0.0;
+    const double rmse = cnt > 0 ? sqrt(tot[28] / cnt) : 0.0;
+    bool done = false;
+    if (pass >= 1 && fabs(P.prev_fitness - fitness) < prm.rel_fit &&
+        fabs(P.prev_rmse - rmse) < prm.rel_rmse)
+        done = true;
+    else if (pass >= prm.max_iter)
+        done = true;
+    P.fitness = fitness;
+    P.rmse = rmse;
+    P.ncorr = int32_t(cnt);
+    if (done) {
+        P.active = 0;
+        return;
+    }
+    double D[16];
+    if (cnt <= 0) {
+        for (int k = 0; k < 16; ++k) D[k] = (k % 5 == 0) ? 1.0 : 0.0;
+    } else if (prm.method == LSM_P2PLANE) {
+        double A[6][6], b[6], x[6];
+        int k = 0;
+        for (int a = 0; a < 6; ++a)
+            for (int c = a; c < 6; ++c) {
+                A[a][c] = tot[k];
+                A[c][a] = tot[k];
+                ++k;
+            }
+        for (int a = 0; a < 6; ++a) b[a] = -tot[21 + a];
+        ldlt_solve6(A, b, x);
+        vec6_to_mat4(x, D);
+    } else {
+        umeyama_update(tot, D);
+    }
+    double T[16];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) {
+            double s = 0.0;
+            for (int k = 0; k < 4; ++k) s += D[4 * r + k] * P.T[4 * k + c];
+            T[4 * r + c] = s;
+        }
+    for (int k = 0; k < 16; ++k) P.T[k] = T[k];
+    P.iter = pass + 1;
+    P.prev_fitness = fitness;
+    P.prev_rmse = rmse;
+    atomicAdd(active_next, 1u);
+    atomicAdd(bytes_next, pair_bytes[blockIdx.x]);
+}
+
+// copy a pair's final correspondences (reference order) for lsm_icp_last_correspondences
+__global__ void corr_to_ref(const int32_t *corr, int n, const uint32_t *src_perm,
+                            const uint32_t *tgt_perm, int64_t *out, uint32_t *count) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int c = corr[i];
+    if (c < 0) return;
+    const uint32_t slot = atomicAdd(count, 1u);
+    out[2 * slot] = src_perm[i];
+    out[2 * slot + 1] = tgt_perm[c];
+}
+
+template <typename T>
+int upload(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out) {
+    T *d = static_cast<T *>(ctx->buf(name, std::max<size_t>(v.size(), 1) * sizeof(T)));
+    if (!d) {
+        ctx->set_error(std::string("scratch allocation failed: ") + name);
+        return LSM_ENOMEM;
+    }
+    if (!v.empty())
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice,
+                                        ctx->stream));
+    *out = d;
+    return LSM_OK;
+}
+
+}  // namespace
+
+int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const double *init,
+                const lsm_icp_params &p, lsm_icp_result *out) {
+    hipStream_t st = ctx->stream;
+    int rc;
+    // unique clouds -> CloudDev table
+    std::vector<Cloud *> uniq;
+    std::vector<int32_t> si(npairs), ti(npairs);
+    auto slot_of = [&](Cloud *c) {
+        for (size_t k = 0; k < uniq.size(); ++k)
+            if (uniq[k] == c) return int32_t(k);
+        uniq.push_back(c);
+        return int32_t(uniq.size() - 1);
+    };
+    if (npairs > 64) {
+        // hash lookup for big batches
+        std::unordered_map<Cloud *, int32_t> m;
+        for (int64_t k = 0; k < npairs; ++k) {
+            for (Cloud *c : {src[k], tgt[k]})
+                if (!m.count(c)) {
+                    m[c] = int32_t(uniq.size());
+                    uniq.push_back(c);
+                }
+            si[k] = m[src[k]];
+            ti[k] = m[tgt[k]];
+        }
+    } else {
+        for (int64_t k = 0; k < npairs; ++k) {
+            si[k] = slot_of(src[k]);
+            ti[k] = slot_of(tgt[k]);
+        }
+    }
+    std::vector<CloudDev> cdev(uniq.size());
+    for (size_t k = 0; k < uniq.size(); ++k) cdev[k] = uniq[k]->dev;
+
+    // pair states, block tasks (XCD-grouped: all blocks of a pair on one XCD's L2)
+    std::vector<PairState> ps(npairs);
+    std::vector<double> pbytes(npairs);
+    std::vector<std::vector<BlockTask>> lane_tasks(NXCD);
+    std::vector<int64_t> lane_load(NXCD, 0);
+    int64_t src_off = 0;
+    int32_t slot = 0;
+    double bytes0 = 0.0;
+    for (int64_t k = 0; k < npairs; ++k) {
+        PairState &P = ps[k];
+        std::memset(&P, 0, sizeof(P));
+        if (init) std::memcpy(P.T, init + 16 * k, 16 * sizeof(double));
+        else
+            for (int q = 0; q < 16; ++q) P.T[q] = (q % 5 == 0) ? 1.0 : 0.0;
+        const int nsrc = int(src[k]->n);
+        P.active = 1;
+        P.nsrc = nsrc;
+        P.src = si[k];
+        P.tgt = ti[k];
+        P.src_off = src_off;
+        const int nblk = (nsrc + NN_THREADS - 1) / NN_THREADS;
+        P.blk0 = slot;
+        P.nblk = nblk;
+        int lane = int(std::min_element(lane_load.begin(), lane_load.end()) - lane_load.begin());
+        for (int b = 0; b < nblk; ++b) lane_tasks[lane].push_back({int32_t(k), b * NN_THREADS, slot + b, 0});
+        lane_load[lane] += nblk;
+        slot += nblk;
+        src_off += nsrc;
+        // SURVEY.md §8d algorithmic bytes of one NN pass of this pair
+        pbytes[k] = double(nsrc) * 12.0 + double(tgt[k]->n) * 12.0 +
+                    double(tgt[k]->nonempty_cells) * 8.0 + double(nsrc) * 8.0;
+        bytes0 += pbytes[k];
+        if (nsrc == 0) {
+            P.nblk = 0;
+        }
+    }
+    // interleave lanes: physical block b -> lane b % 8 (round-robin XCD dispatch)
+    size_t maxlen = 0;
+    for (auto &l : lane_tasks) maxlen = std::max(maxlen, l.size());
+    std::vector<BlockTask> tasks;
+    tasks.reserve(maxlen * NXCD);
+    for (size_t m = 0; m < maxlen; ++m)
+        for (int l = 0; l < NXCD; ++l)
+            tasks.push_back(m < lane_tasks[l].size() ? lane_tasks[l][m] : BlockTask{-1, 0, 0, 0});
+    // trim trailing padding
+    while (!tasks.empty() && tasks.back().pair < 0) tasks.pop_back();
+    const int ntasks = int(tasks.size());
+    const int max_iter = p.max_iteration;
+
+    CloudDev *d_cd;
+    PairState *d_ps;
+    BlockTask *d_tasks;
+    double *d_pbytes;
+    if ((rc = upload(ctx, "i_cd", cdev, &d_cd))) return rc;
+    if ((rc = upload(ctx, "i_ps", ps, &d_ps))) return rc;
+    if ((rc = upload(ctx, "i_tasks", tasks, &d_tasks))) return rc;
+    if ((rc = upload(ctx, "i_pbytes", pbytes, &d_pbytes))) return rc;
+    const size_t nsrc_tot = size_t(std::max<int64_t>(src_off, 1));
+    int32_t *d_corr = (int32_t *)ctx->buf("i_corr", nsrc_tot * 4);
+    float *d_cd2 = (float *)ctx->buf("i_cd2", nsrc_tot * 4);
+    const uint32_t qcap = uint32_t(nsrc_tot);
+    FallbackItem *d_q = (FallbackItem *)ctx->buf("i_queue", size_t(qcap) * sizeof(FallbackItem));
+    double *d_part = (double *)ctx->buf("i_part", size_t(std::max(slot, 1)) * LSM_ACC * 8);
+    const int ncnt = max_iter + 2;
+    uint32_t *d_counters = (uint32_t *)ctx->buf("i_counters", size_t(ncnt) * 2 * 4);
+    double *d_bytes = (double *)ctx->buf("i_bytes", size_t(ncnt) * 8);
+    if (!d_corr || !d_cd2 || !d_q || !d_part || !d_counters || !d_bytes) {
+        ctx->set_error("scratch allocation failed (icp)");
+        return LSM_ENOMEM;
+    }
+    uint32_t *d_qn = d_counters;            // [ncnt] fallback queue sizes per pass
+    uint32_t *d_active = d_counters + ncnt; // [ncnt] active pairs after each pass
+    LSM_HIP_TRY(ctx, hipMemsetAsync(d_counters, 0, size_t(ncnt) * 2 * 4, st));
+    LSM_HIP_TRY(ctx, hipMemsetAsync(d_bytes, 0, size_t(ncnt) * 8, st));
+    if (src_off > 0) LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
+
+    NNParams prm;
+    prm.maxc = float(p.max_correspondence_distance);
+    prm.maxc2 = float(p.max_correspondence_distance * p.max_correspondence_distance);
+    prm.method = p.method;
+    prm.max_iter = max_iter;
+    prm.rel_fit = p.relative_fitness;
+    prm.rel_rmse = p.relative_rmse;
+
+    uint32_t *h_active = (uint32_t *)ctx->host_pinned(64);
+    if (!h_active) return LSM_ENOMEM;
+    double nn_bytes = bytes0;
+    const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
+    for (int pass = 0; pass <= max_iter && ntasks > 0; ++pass) {
+        hipEvent_t ev;
+        ctx->tic("nn", &ev);
+        nn_kernel<<<ntasks, NN_THREADS, 0, st>>>(d_tasks, d_ps, d_cd, prm, d_corr, d_cd2, d_q,
+                                                 d_qn + pass, qcap);
+        ctx->toc("nn", ev);
+        ctx->tic("nn_fallback", &ev);
+        nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass, qcap, d_corr,
+                                                  d_cd2);
+        ctx->toc("nn_fallback", ev);
+        ctx->tic("accumulate", &ev);
+        if (p.method == LSM_P2PLANE)
+            accumulate_kernel<LSM_P2PLANE><<<ntasks, NN_THREADS, 0, st>>>(d_tasks, d_ps, d_cd,
+                                                                          d_corr, d_part);
+        else
+            accumulate_kernel<LSM_P2P><<<ntasks, NN_THREADS, 0, st>>>(d_tasks, d_ps, d_cd, d_corr,
+                                                                      d_part);
+        ctx->toc("accumulate", ev);
+        ctx->tic("solve", &ev);
+        solve_kernel<<<int(npairs), LSM_WAVE, 0, st>>>(d_ps, d_part, prm, pass, d_pbytes,
+                                                       d_active + pass, d_bytes + pass);
+        ctx->toc("solve", ev);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(h_active, d_active + pass, 4, hipMemcpyDeviceToHost, st));
+        double hb = 0.0;
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(h_active + 2, d_bytes + pass, 8, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        std::memcpy(&hb, h_active + 2, 8);
+        if (h_active[0] == 0) break;
+        nn_bytes += hb;
+    }
+    LSM_HIP_TRY(ctx, hipGetLastError());
+    // results
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(ps.data(), d_ps, ps.size() * sizeof(PairState),
+                                    hipMemcpyDeviceToHost, st));
+    // pair 0 correspondences in reference order
+    {
+        const int n0 = int(src[0]->n);
+        int64_t *d_lc = (int64_t *)ctx->buf("i_lastcorr", size_t(std::max(n0, 1)) * 16);
+        uint32_t *d_lcn = (uint32_t *)ctx->buf("i_lastcorr_n", 16);
+        if (!d_lc || !d_lcn) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_lcn, 0, 4, st));
+        if (n0 > 0)
+            corr_to_ref<<<(n0 + 255) / 256, 256, 0, st>>>(d_corr, n0, src[0]->d_perm,
+                                                         tgt[0]->d_perm, d_lc, d_lcn);
+        uint32_t m = 0;
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(&m, d_lcn, 4, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        ctx->last_corr.resize(size_t(m) * 2);
+        if (m)
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(ctx->last_corr.data(), d_lc, size_t(m) * 16,
+                                            hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        // deterministic order: by source index
+        std::vector<std::pair<int64_t, int64_t>> v(m);
+        for (uint32_t k = 0; k < m; ++k) v[k] = {ctx->last_corr[2 * k], ctx->last_corr[2 * k + 1]};
+        std::sort(v.begin(), v.end());
+        for (uint32_t k = 0; k < m; ++k) {
+            ctx->last_corr[2 * k] = v[k].first;
+            ctx->last_corr[2 * k + 1] = v[k].second;
+        }
+    }
+    ctx->collect_timings();
+    if (ctx->timing) ctx->stats["nn"].algo_bytes += nn_bytes;
+    for (int64_t k = 0; k < npairs; ++k) {
+        const PairState &P = ps[k];
+        lsm_icp_result &R = out[k];
+        std::memcpy(R.transformation, P.T, sizeof(R.transformation));
+        R.fitness = P.fitness;
+        R.inlier_rmse = P.rmse;
+        R.correspondences = P.ncorr;
+        R.iterations = P.iter;
+        R.status = 0;
+    }
+    return LSM_OK;
+}

@@ -1,0 +1,87 @@
+// lsm_common.h -- shared device/host structures of liblidarsm (gfx950 / CDNA4 only).
+//
+// Data layout in HBM:
+//   * every processed keyframe cloud is stored cell-sorted: points float4 (x, y, z, 0) ordered
+//     by the linear index of a uniform grid cell (z-major, then y, then x), so the 3 cells of a
+//     grid row are ONE contiguous point range, and a workgroup of consecutive points covers a
+//     compact patch of space (coherent queries when the cloud is an ICP source);
+//   * a dense CSR cell table cell_start[nx*ny*nz + 1] (u32) over the cloud's own bounding box;
+//   * normals float4 in the same order; perm[] maps sorted position -> reference (filter) order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#define LSM_WAVE 64
+
+// Device descriptor of one processed cloud (POD; an array of these lives in device memory).
+struct CloudDev {
+    const float4 *xyz;          // n, cell-sorted
+    const float4 *nrm;          // n or nullptr
+    const uint32_t *cell_start; // ncells + 1, offsets into xyz
+    float ox, oy, oz;           // grid origin
+    float cell, inv_cell;       // cell edge and its reciprocal
+    int nx, ny, nz;
+    int n;
+};
+
+// Per-pair ICP state (device). Layout kept 8-byte aligned.
+struct PairState {
+    double T[16];        // current transformation (row-major), f64 as Open3D
+    double fitness, rmse;
+    double prev_fitness, prev_rmse;
+    int32_t iter;        // updates applied
+    int32_t active;      // 1 while the pair still runs correspondence passes
+    int32_t ncorr;       // correspondences of the latest pass
+    int32_t nsrc;        // source points (fitness denominator)
+    int32_t src, tgt;    // indices into the CloudDev table of this batch
+    int32_t blk0, nblk;  // first logical partial slot and number of source blocks
+    int64_t src_off;     // offset of this pair's source points in the batch corr arrays
+};
+
+// Logical block -> (pair, first source point) for pair-indexed grids.
+struct BlockTask {
+    int32_t pair;   // -1 = padding (XCD balancing)
+    int32_t start;  // first source point of this block
+    int32_t slot;   // partial-sum slot (pair's blk0 + k)
+    int32_t pad;
+};
+
+// Accumulator layout of the ICP reduction (f64): see icp.hip.
+#define LSM_ACC 32
+
+// ----------------------------------------------------------------------------------------------
+// Host-side helpers
+// ----------------------------------------------------------------------------------------------
+#define LSM_HIP_TRY(ctx, expr)                                                          \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess) {                                                         \
+            (ctx)->set_error(std::string(#expr) + ": " + hipGetErrorString(_e));        \
+            return LSM_EHIP;                                                            \
+        }                                                                               \
+    } while (0)
+
+// Exact nanoflann-style squared distance in f64 without contraction:
+// ((dx*dx + dy*dy) + dz*dz), dx = q - p (L2_Adaptor::evalMetric order).
+__device__ __forceinline__ double lsm_sqdist64(double qx, double qy, double qz, double px,
+                                               double py, double pz) {
+    double dx = __dsub_rn(qx, px), dy = __dsub_rn(qy, py), dz = __dsub_rn(qz, pz);
+    return __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+}
+
+__device__ __forceinline__ int lsm_clampi(int v, int lo, int hi) {
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// Wave-wide sum of a double (64 lanes, fixed tree -> deterministic).
+__device__ __forceinline__ double lsm_wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, LSM_WAVE);
+    return v;
+}
+
+// Kernel launchers implemented in the .hip translation units (all on `s`).
+struct PrepBatch;  // defined in prep.hip

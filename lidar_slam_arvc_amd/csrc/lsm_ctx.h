@@ -1,0 +1,92 @@
+// lsm_ctx.h -- host-side context of liblidarsm: device buffers, clouds, instrumentation.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/lidarsm.h"
+#include "lsm_common.h"
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+// One keyframe cloud resident on the device (the keyframe cache, SURVEY.md §8b "Ownership").
+struct Cloud {
+    int64_t n_raw = 0;
+    float *d_raw = nullptr;       // n_raw x 3 float32 (as uploaded, reference order)
+    int64_t cap = 0;              // capacity of the processed arrays (points)
+    int64_t n = 0;                // processed points
+    float4 *d_xyz = nullptr;      // cell-sorted points
+    float4 *d_nrm = nullptr;      // cell-sorted normals
+    uint32_t *d_perm = nullptr;   // sorted position -> reference-order index
+    uint32_t *d_cell = nullptr;   // cell_start table
+    int64_t cell_cap = 0;
+    double *d_vox = nullptr;      // voxel centroids (f64, voxel-key order), voxelised clouds only
+    int32_t *d_vkeys = nullptr;   // voxel keys (int32 x 3)
+    int64_t vox_cap = 0;
+    bool processed = false;
+    bool has_normals = false;
+    bool voxelized = false;
+    int64_t nonempty_cells = 0;
+    CloudDev dev{};               // host copy of the device descriptor
+};
+
+struct KStat {
+    int64_t launches = 0;
+    double ms = 0.0;
+    double algo_bytes = 0.0;
+};
+
+struct lsm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::unordered_map<int64_t, Cloud *> clouds;
+    int64_t next_id = 1;
+    std::map<std::string, DevBuf> scratch;
+    void *pinned = nullptr;       // small pinned staging area for counters
+    size_t pinned_bytes = 0;
+    int num_cus = 256;
+
+    // instrumentation
+    bool timing = false;
+    std::map<std::string, KStat> stats;
+    struct Pending {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+
+    // last correspondence set (reference order) of pair 0 of the last ICP call
+    std::vector<int64_t> last_corr;
+
+    void set_error(const std::string &e) { err = e; }
+    // grow-only named scratch buffer
+    void *buf(const std::string &name, size_t bytes);
+    void *host_pinned(size_t bytes);
+    hipEvent_t get_event();
+    // bracket a launch with events when timing is on
+    void tic(const char *name, hipEvent_t *a);
+    void toc(const char *name, hipEvent_t a);
+    void collect_timings();   // call after the stream is synchronised
+};
+
+// ------------------------------------------------------------------------------------------
+// Internal entry points (implemented per translation unit)
+// ------------------------------------------------------------------------------------------
+int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params &p,
+                   int64_t *n_out);
+int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const double *init,
+                const lsm_icp_params &p, lsm_icp_result *out);
+int lsm_loop_candidates_run(lsm_ctx *ctx, const double *positions, int64_t m, double dback,
+                            double radius, int64_t *index_backwards, int64_t *cand, int64_t cap,
+                            int64_t *ncand);
+int lsm_loop_partners_run(lsm_ctx *ctx, const double *positions, int64_t m,
+                          const int64_t *cand, int64_t ncand, int64_t *partner);
+int lsm_download_run(lsm_ctx *ctx, Cloud *c, double *xyz, double *nrm, int64_t cap);

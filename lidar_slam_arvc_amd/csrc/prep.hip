@@ -1,0 +1,1075 @@
+// prep.hip -- KeyFrame.pre_process on the device (keyframe.py:113-124), batched over keyframes.
+//
+//   filter_radius_height  (keyframe.py:74-94)        : f64 strict mask + order-preserving compaction
+//   voxel_down_sample     (keyframe.py:150-151)      : f64 Open3D voxel keys, stable sort, per-voxel
+//                                                      sequential f64 mean (bit-exact with Open3D)
+//   spatial index (replaces KDTreeFlann)             : cell keys -> radix sort -> dense CSR table
+//   estimate_normals      (keyframe.py:160-162)      : hybrid radius / kNN-300 neighbourhoods,
+//                                                      exact f64 distances, FastEigen3x3
+//
+// All kernels of a stage run over every keyframe of the batch in one launch (block tables map
+// workgroups to (keyframe, first point)); the host synchronises only to learn data-dependent
+// point counts (filter, voxel) and grid extents.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <vector>
+
+#include "fasteigen.h"
+#include "lsm_ctx.h"
+
+namespace {
+
+constexpr int FILTER_THREADS = 256;
+constexpr int FILTER_PER_THREAD = 4;
+constexpr int FILTER_CHUNK = FILTER_THREADS * FILTER_PER_THREAD;
+constexpr int PT_THREADS = 256;
+constexpr int64_t MAX_CELLS_PER_CLOUD = int64_t(1) << 24;
+
+struct Seg {           // (keyframe, first point) of one workgroup
+    int32_t cloud;
+    int32_t start;
+};
+
+// ------------------------------------------------------------------------------------------
+// filter_radius_height: keep iff x^2+y^2 < maxr^2, > minr^2, z > minh, z < maxh (all strict,
+// float64, no FMA contraction -- numpy evaluates x**2 + y**2 as two rounded products and a sum).
+// ------------------------------------------------------------------------------------------
+struct FilterParams {
+    double maxr2, minr2, minh, maxh;
+};
+
+__device__ __forceinline__ bool keep_point(float x, float y, float z, const FilterParams &f) {
+    double dx = x, dy = y, dz = z;
+    double r2 = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+    return (r2 < f.maxr2) & (r2 > f.minr2) & (dz > f.minh) & (dz < f.maxh);
+}
+
+__global__ void __launch_bounds__(FILTER_THREADS)
+filter_count(const Seg *segs, const float *const *raw, const int32_t *nraw, FilterParams f,
+             uint32_t *bcount) {
+    const Seg s = segs[blockIdx.x];
+    const float *p = raw[s.cloud];
+    const int n = nraw[s.cloud];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < FILTER_PER_THREAD; ++k) {
+        int i = s.start + k * FILTER_THREADS + threadIdx.x;
+        if (i < n) c += keep_point(p[3 * i], p[3 * i + 1], p[3 * i + 2], f) ? 1u : 0u;
+    }
+    // wave sum then LDS across 4 waves
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, LSM_WAVE);
+    __shared__ uint32_t ws[FILTER_THREADS / LSM_WAVE];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < FILTER_THREADS / LSM_WAVE; ++w) t += ws[w];
+        bcount[blockIdx.x] = t;
+    }
+}
+
+// Order-preserving compaction: within a block, points are handled in index order (k-major
+// chunks of 256), ranks from wave ballots + LDS prefix of wave totals.
+__global__ void __launch_bounds__(FILTER_THREADS)
+filter_write(const Seg *segs, const float *const *raw, const int32_t *nraw, FilterParams f,
+             const uint32_t *boff, float4 *out, uint32_t *src_index) {
+    const Seg s = segs[blockIdx.x];
+    const float *p = raw[s.cloud];
+    const int n = nraw[s.cloud];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ uint32_t wtot[FILTER_THREADS / LSM_WAVE];
+    uint32_t base = boff[blockIdx.x];
+    for (int k = 0; k < FILTER_PER_THREAD; ++k) {
+        int i = s.start + k * FILTER_THREADS + threadIdx.x;
+        float x = 0.f, y = 0.f, z = 0.f;
+        bool keep = false;
+        if (i < n) {
+            x = p[3 * i];
+            y = p[3 * i + 1];
+            z = p[3 * i + 2];
+            keep = keep_point(x, y, z, f);
+        }
+        uint64_t m = __ballot(keep);
+        uint32_t below = __popcll(m & ((uint64_t(1) << lane) - 1));
+        if (lane == 0) wtot[wave] = __popcll(m);
+        __syncthreads();
+        uint32_t woff = 0, tot = 0;
+        for (int w = 0; w < FILTER_THREADS / LSM_WAVE; ++w) {
+            woff += (w < wave) ? wtot[w] : 0u;
+            tot += wtot[w];
+        }
+        if (keep) {
+            uint32_t o = base + woff + below;
+            out[o] = make_float4(x, y, z, 0.f);
+            src_index[o] = uint32_t(i);
+        }
+        base += tot;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// bounding boxes (f64 for the voxel grid, f32 values are exact in f64)
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+bbox_kernel(const float4 *pts, const uint32_t *cloud_off, const uint32_t *cloud_n, double *bb) {
+    const int c = blockIdx.x;
+    const uint32_t off = cloud_off[c], n = cloud_n[c];
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        float4 p = pts[off + i];
+        mn[0] = fmin(mn[0], (double)p.x);
+        mn[1] = fmin(mn[1], (double)p.y);
+        mn[2] = fmin(mn[2], (double)p.z);
+        mx[0] = fmax(mx[0], (double)p.x);
+        mx[1] = fmax(mx[1], (double)p.y);
+        mx[2] = fmax(mx[2], (double)p.z);
+    }
+    __shared__ double red[6][256];
+    for (int k = 0; k < 3; ++k) {
+        red[k][threadIdx.x] = mn[k];
+        red[3 + k][threadIdx.x] = mx[k];
+    }
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            for (int k = 0; k < 3; ++k) {
+                red[k][threadIdx.x] = fmin(red[k][threadIdx.x], red[k][threadIdx.x + s]);
+                red[3 + k][threadIdx.x] = fmax(red[3 + k][threadIdx.x], red[3 + k][threadIdx.x + s]);
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) bb[6 * c + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// ------------------------------------------------------------------------------------------
+// voxel_down_sample ([O3D] PointCloud::VoxelDownSample)
+// ------------------------------------------------------------------------------------------
+struct VoxGeo {         // per cloud, computed on the host from the f64 bbox
+    double ox, oy, oz;  // voxel_min_bound = min_bound - v/2
+    int64_t dx, dy, dz; // key extents
+    uint64_t key_off;   // offset of this cloud in the global key space
+};
+
+__global__ void __launch_bounds__(PT_THREADS)
+voxel_keys(const Seg *segs, const float4 *pts, const uint32_t *cloud_off, const uint32_t *cloud_n,
+           const VoxGeo *geo, double v, uint64_t *keys, uint32_t *vals) {
+    const Seg s = segs[blockIdx.x];
+    const int i = s.start + threadIdx.x;
+    if (i >= int(cloud_n[s.cloud])) return;
+    const uint32_t g = cloud_off[s.cloud] + i;
+    const VoxGeo G = geo[s.cloud];
+    float4 p = pts[g];
+    // ref_coord = (p - voxel_min_bound) / voxel_size ; voxel_index = int(floor(ref_coord))
+    int64_t kx = (int64_t)(int)floor(__ddiv_rn(__dsub_rn((double)p.x, G.ox), v));
+    int64_t ky = (int64_t)(int)floor(__ddiv_rn(__dsub_rn((double)p.y, G.oy), v));
+    int64_t kz = (int64_t)(int)floor(__ddiv_rn(__dsub_rn((double)p.z, G.oz), v));
+    keys[g] = G.key_off + uint64_t((kx * G.dy + ky) * G.dz + kz);
+    vals[g] = g;
+}
+
+// One thread per sorted entry; voxel heads sum their members in index order (stable sort keeps
+// the original order inside a voxel) exactly like AccumulatedPoint::AddPoint.
+__global__ void __launch_bounds__(PT_THREADS)
+voxel_flags(const uint64_t *skeys, uint32_t n, uint32_t *flag) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    flag[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(PT_THREADS)
+voxel_reduce(const uint64_t *skeys, const uint32_t *svals, const uint32_t *vid_excl,
+             const uint32_t *flag, uint32_t n, const float4 *pts, const int32_t *pt_cloud,
+             const VoxGeo *geo, double *cent, int32_t *vkeys, float4 *vpts, int32_t *vcloud) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    const uint64_t key = skeys[i];
+    double sx = 0.0, sy = 0.0, sz = 0.0;
+    uint32_t j = i;
+    for (; j < n && skeys[j] == key; ++j) {
+        float4 p = pts[svals[j]];
+        sx = __dadd_rn(sx, (double)p.x);
+        sy = __dadd_rn(sy, (double)p.y);
+        sz = __dadd_rn(sz, (double)p.z);
+    }
+    const double cnt = double(j - i);
+    const uint32_t o = vid_excl[i];
+    const double cx = __ddiv_rn(sx, cnt), cy = __ddiv_rn(sy, cnt), cz = __ddiv_rn(sz, cnt);
+    cent[3 * o] = cx;
+    cent[3 * o + 1] = cy;
+    cent[3 * o + 2] = cz;
+    const int c = pt_cloud[svals[i]];
+    const VoxGeo G = geo[c];
+    const uint64_t local = key - G.key_off;
+    const int64_t kz = int64_t(local % uint64_t(G.dz));
+    const int64_t ky = int64_t((local / uint64_t(G.dz)) % uint64_t(G.dy));
+    const int64_t kx = int64_t(local / uint64_t(G.dz * G.dy));
+    vkeys[3 * o] = int32_t(kx);
+    vkeys[3 * o + 1] = int32_t(ky);
+    vkeys[3 * o + 2] = int32_t(kz);
+    vpts[o] = make_float4(float(cx), float(cy), float(cz), 0.f);
+    vcloud[o] = c;
+}
+
+__global__ void point_cloud_ids(const uint32_t *cloud_off, const uint32_t *cloud_n, int ncloud,
+                                int32_t *pt_cloud) {
+    int c = blockIdx.y;
+    if (c >= ncloud) return;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cloud_n[c];
+         i += gridDim.x * blockDim.x)
+        pt_cloud[cloud_off[c] + i] = c;
+}
+
+// ------------------------------------------------------------------------------------------
+// spatial index: global cell key per point, radix sort, gather, dense CSR cell table
+// ------------------------------------------------------------------------------------------
+struct GridGeo {
+    float ox, oy, oz, cell, inv_cell;
+    int nx, ny, nz;
+    uint32_t cell_off;     // offset of this cloud in the global cell space
+    uint32_t pt_off;       // offset of this cloud in the batch point arrays
+    uint32_t n;
+    uint32_t pad;
+};
+
+__device__ __forceinline__ int cell_coord(float v, float o, float inv, int nmax) {
+    return lsm_clampi((int)floorf((v - o) * inv), 0, nmax - 1);
+}
+
+__global__ void __launch_bounds__(PT_THREADS)
+grid_keys(const Seg *segs, const float4 *pts, const GridGeo *geo, uint32_t *keys,
+          uint32_t *vals) {
+    const Seg s = segs[blockIdx.x];
+    const GridGeo G = geo[s.cloud];
+    const int i = s.start + threadIdx.x;
+    if (i >= int(G.n)) return;
+    const uint32_t g = G.pt_off + i;
+    float4 p = pts[g];
+    int cx = cell_coord(p.x, G.ox, G.inv_cell, G.nx);
+    int cy = cell_coord(p.y, G.oy, G.inv_cell, G.ny);
+    int cz = cell_coord(p.z, G.oz, G.inv_cell, G.nz);
+    keys[g] = G.cell_off + uint32_t((cz * G.ny + cy) * G.nx + cx);
+    vals[g] = g;
+}
+
+__global__ void __launch_bounds__(PT_THREADS)
+grid_scatter(const Seg *segs, const GridGeo *geo, const CloudDev *cd, const uint32_t *svals,
+             const uint32_t *skeys, const float4 *pts, uint32_t *const *perm_out,
+             uint32_t *nonempty) {
+    const Seg s = segs[blockIdx.x];
+    const GridGeo G = geo[s.cloud];
+    const int j = s.start + threadIdx.x;
+    bool head = false;
+    if (j < int(G.n)) {
+        const uint32_t g = G.pt_off + j;
+        const uint32_t v = svals[g];
+        float4 *xyz = const_cast<float4 *>(cd[s.cloud].xyz);
+        xyz[j] = pts[v];
+        perm_out[s.cloud][j] = v - G.pt_off;   // reference (filter / voxel-key) order
+        head = (j == 0) || (skeys[g] != skeys[g - 1]);
+    }
+    uint64_t m = __ballot(head);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&nonempty[s.cloud], (uint32_t)__popcll(m));
+}
+
+// cell_start[c] = first sorted position with key >= c (lower bound), for c in [0, ncells].
+// One thread per chunk of 32 cells: one binary search, then a merge-walk.
+constexpr int FILL_CHUNK = 32;
+
+__global__ void __launch_bounds__(256)
+grid_fill(const GridGeo *geo, int ncloud, const uint32_t *skeys, uint32_t *const *cell_out) {
+    // blockIdx.y = cloud
+    const int c = blockIdx.y;
+    if (c >= ncloud) return;
+    const GridGeo G = geo[c];
+    const int64_t ncells = int64_t(G.nx) * G.ny * G.nz;
+    const int64_t nchunks = (ncells + 1 + FILL_CHUNK - 1) / FILL_CHUNK;
+    uint32_t *out = cell_out[c];
+    const uint32_t *k = skeys + G.pt_off;
+    for (int64_t ch = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; ch < nchunks;
+         ch += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t c0 = ch * FILL_CHUNK;
+        // lower_bound of (cell_off + c0)
+        uint32_t lo = 0, hi = G.n;
+        const uint32_t target = G.cell_off + uint32_t(c0);
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (k[mid] < target) lo = mid + 1;
+            else hi = mid;
+        }
+        uint32_t j = lo;
+        const int64_t c1 = c0 + FILL_CHUNK < ncells + 1 ? c0 + FILL_CHUNK : ncells + 1;
+        for (int64_t cc = c0; cc < c1; ++cc) {
+            const uint32_t t = G.cell_off + uint32_t(cc);
+            while (j < G.n && k[j] < t) ++j;
+            out[cc] = j;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// normals: KDTreeSearchParamHybrid(radius, max_nn) neighbourhoods on the cell grid
+// ------------------------------------------------------------------------------------------
+struct NormalParams {
+    double r2;        // radius^2 in f64 (Open3D compares d^2 < radius*radius)
+    float r;          // radius (search box half-width)
+    int max_nn;
+};
+
+// Covariance from centred cumulants (mathematically identical to Open3D's raw cumulants;
+// centring on the query point avoids f64 cancellation at 35 m coordinates).
+struct Cum {
+    double sx, sy, sz, sxx, sxy, sxz, syy, syz, szz;
+    int n;
+};
+
+__device__ __forceinline__ void cum_add(Cum &c, double dx, double dy, double dz) {
+    c.sx += dx;
+    c.sy += dy;
+    c.sz += dz;
+    c.sxx += dx * dx;
+    c.sxy += dx * dy;
+    c.sxz += dx * dz;
+    c.syy += dy * dy;
+    c.syz += dy * dz;
+    c.szz += dz * dz;
+    c.n += 1;
+}
+
+__device__ __forceinline__ float4 normal_from_cum(const Cum &c) {
+    sym3 A;
+    if (c.n >= 3) {
+        const double inv = 1.0 / double(c.n);
+        const double mx = c.sx * inv, my = c.sy * inv, mz = c.sz * inv;
+        A.a00 = c.sxx * inv - mx * mx;
+        A.a11 = c.syy * inv - my * my;
+        A.a22 = c.szz * inv - mz * mz;
+        A.a01 = c.sxy * inv - mx * my;
+        A.a02 = c.sxz * inv - mx * mz;
+        A.a12 = c.syz * inv - my * mz;
+    } else {
+        A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+    }
+    d3 v = fast_eigen3x3_min(A);
+    if (sqrt(d3_dot(v, v)) == 0.0) v = {0.0, 0.0, 1.0};
+    return make_float4(float(v.x), float(v.y), float(v.z), 0.f);
+}
+
+// Cell range of [q - h, q + h] along one axis, widened by a small margin so every point within
+// L-inf distance h is covered despite f32 rounding of the cell coordinate.
+__device__ __forceinline__ void axis_range(float q, float o, float inv, float h, int nmax, int &lo,
+                                           int &hi) {
+    float a = (q - o) * inv;
+    float hh = h * inv;
+    lo = (int)floorf(a - hh - 1e-3f);
+    hi = (int)floorf(a + hh + 1e-3f);
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > nmax - 1 ? nmax - 1 : hi;
+}
+
+// squared distance from coordinate q to the cell slab [o + k*c, o + (k+1)*c) (0 inside)
+__device__ __forceinline__ float slab_d2(float q, float o, float c, int k) {
+    float lo = o + k * c, hi = lo + c;
+    float d = q < lo ? lo - q : (q > hi ? q - hi : 0.f);
+    return d * d;
+}
+
+__global__ void __launch_bounds__(PT_THREADS)
+normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *overflow,
+               uint32_t *overflow_n, uint32_t overflow_cap) {
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int j = s.start + threadIdx.x;
+    if (j >= C.n) return;
+    const float4 qf = C.xyz[j];
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    int xlo, xhi, ylo, yhi, zlo, zhi;
+    axis_range(qf.x, C.ox, C.inv_cell, np.r, C.nx, xlo, xhi);
+    axis_range(qf.y, C.oy, C.inv_cell, np.r, C.ny, ylo, yhi);
+    axis_range(qf.z, C.oz, C.inv_cell, np.r, C.nz, zlo, zhi);
+    const float prune = np.r * 1.0001f + 1e-6f;
+    const float prune2 = prune * prune;
+    Cum c = {};
+    for (int z = zlo; z <= zhi; ++z) {
+        const float dz2 = slab_d2(qf.z, C.oz, C.cell, z);
+        if (dz2 > prune2) continue;
+        for (int y = ylo; y <= yhi; ++y) {
+            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
+            if (dyz2 > prune2) continue;
+            const int row = (z * C.ny + y) * C.nx;
+            const uint32_t a = C.cell_start[row + xlo], b = C.cell_start[row + xhi + 1];
+            for (uint32_t k = a; k < b; ++k) {
+                const float4 p = C.xyz[k];
+                const double d2 = lsm_sqdist64(qx, qy, qz, p.x, p.y, p.z);
+                if (d2 < np.r2) cum_add(c, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
+            }
+        }
+    }
+    if (c.n > np.max_nn) {
+        uint32_t slot = atomicAdd(overflow_n, 1u);
+        if (slot < overflow_cap) {
+            overflow[slot] = uint32_t(s.cloud);
+            overflow[overflow_cap + slot] = uint32_t(j);
+        }
+        return;
+    }
+    float4 *nrm = const_cast<float4 *>(C.nrm);
+    nrm[j] = normal_from_cum(c);
+}
+
+// kNN truncation (Open3D SearchHybrid keeps the max_nn nearest): one wave (= one workgroup) per
+// overflowing point. Exact selection of the max_nn smallest (d2, sorted index) pairs: histogram
+// narrowing of a d2 interval [lo, hi) until the boundary bin fits in LDS, then ranking of that
+// bin's members. Bin boundaries are explicit values so the "below the bin" test and the bin
+// membership test agree bit for bit.
+constexpr int OV_BINS = 256;
+constexpr int OV_CAP = 512;
+
+template <typename F>
+__device__ __forceinline__ void scan_ball(const CloudDev &C, float4 qf, float r, int lane, F &&f) {
+    int xlo, xhi, ylo, yhi, zlo, zhi;
+    axis_range(qf.x, C.ox, C.inv_cell, r, C.nx, xlo, xhi);
+    axis_range(qf.y, C.oy, C.inv_cell, r, C.ny, ylo, yhi);
+    axis_range(qf.z, C.oz, C.inv_cell, r, C.nz, zlo, zhi);
+    const float prune = r * 1.0001f + 1e-6f;
+    const float prune2 = prune * prune;
+    for (int z = zlo; z <= zhi; ++z) {
+        const float dz2 = slab_d2(qf.z, C.oz, C.cell, z);
+        if (dz2 > prune2) continue;
+        for (int y = ylo; y <= yhi; ++y) {
+            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
+            if (dyz2 > prune2) continue;
+            const int row = (z * C.ny + y) * C.nx;
+            const uint32_t a = C.cell_start[row + xlo], b = C.cell_start[row + xhi + 1];
+            for (uint32_t k = a + lane; k < b; k += LSM_WAVE) f(k);
+        }
+    }
+}
+
+__device__ __forceinline__ double ov_bound(double lo, double hi, double width, int b) {
+    return b <= 0 ? lo : (b >= OV_BINS ? hi : lo + width * double(b));
+}
+
+__device__ __forceinline__ int ov_bin(double d2, double lo, double hi, double width,
+                                      double scale) {
+    int b = (int)((d2 - lo) * scale);
+    b = b < 0 ? 0 : (b >= OV_BINS ? OV_BINS - 1 : b);
+    while (b > 0 && d2 < ov_bound(lo, hi, width, b)) --b;
+    while (b < OV_BINS - 1 && d2 >= ov_bound(lo, hi, width, b + 1)) ++b;
+    return b;
+}
+
+__global__ void __launch_bounds__(LSM_WAVE)
+normals_overflow(const CloudDev *cd, NormalParams np, const uint32_t *overflow,
+                 const uint32_t *overflow_n, uint32_t overflow_cap) {
+    __shared__ uint32_t hist[OV_BINS];
+    __shared__ double cd2[OV_CAP];
+    __shared__ uint32_t cidx[OV_CAP];
+    __shared__ uint32_t ccnt;
+    const int lane = threadIdx.x;
+    const uint32_t total = min(*overflow_n, overflow_cap);
+    for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
+        const int cloud = int(overflow[item]);
+        const uint32_t j = overflow[overflow_cap + item];
+        const CloudDev C = cd[cloud];
+        const float4 qf = C.xyz[j];
+        const double qx = qf.x, qy = qf.y, qz = qf.z;
+        double lo = 0.0, hi = np.r2;
+        uint32_t need = uint32_t(np.max_nn);  // still to take from [lo, hi)
+        for (int iter = 0; iter < 8; ++iter) {
+            for (int b = lane; b < OV_BINS; b += LSM_WAVE) hist[b] = 0;
+            __syncthreads();
+            const double width = (hi - lo) / double(OV_BINS);
+            const double scale = double(OV_BINS) / (hi - lo);
+            scan_ball(C, qf, np.r, lane, [&](uint32_t k) {
+                const float4 p = C.xyz[k];
+                const double d2 = lsm_sqdist64(qx, qy, qz, p.x, p.y, p.z);
+                if (d2 < np.r2 && d2 >= lo && d2 < hi)
+                    atomicAdd(&hist[ov_bin(d2, lo, hi, width, scale)], 1u);
+            });
+            __syncthreads();
+            int bstar = OV_BINS - 1;
+            uint32_t before = 0;
+            if (lane == 0) {
+                uint32_t acc = 0;
+                for (int b = 0; b < OV_BINS; ++b) {
+                    if (acc + hist[b] >= need) {
+                        bstar = b;
+                        break;
+                    }
+                    acc += hist[b];
+                }
+                before = acc;
+            }
+            bstar = __shfl(bstar, 0, LSM_WAVE);
+            before = __shfl(before, 0, LSM_WAVE);
+            const uint32_t bin_count = hist[bstar];
+            const double nlo = ov_bound(lo, hi, width, bstar);
+            const double nhi = ov_bound(lo, hi, width, bstar + 1);
+            need -= before;
+            lo = nlo;
+            hi = nhi;
+            __syncthreads();
+            if (bin_count <= OV_CAP || !(hi > lo)) break;
+        }
+        // accumulate everything below lo; collect the [lo, hi) members
+        if (lane == 0) ccnt = 0;
+        __syncthreads();
+        Cum c = {};
+        scan_ball(C, qf, np.r, lane, [&](uint32_t k) {
+            const float4 p = C.xyz[k];
+            const double d2 = lsm_sqdist64(qx, qy, qz, p.x, p.y, p.z);
+            if (!(d2 < np.r2)) return;
+            if (d2 < lo) {
+                cum_add(c, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
+            } else if (d2 < hi) {
+                uint32_t slot = atomicAdd(&ccnt, 1u);
+                if (slot < OV_CAP) {
+                    cd2[slot] = d2;
+                    cidx[slot] = k;
+                }
+            }
+        });
+        __syncthreads();
+        const uint32_t m = min(ccnt, (uint32_t)OV_CAP);
+        for (uint32_t e = lane; e < m; e += LSM_WAVE) {
+            const double de = cd2[e];
+            const uint32_t ie = cidx[e];
+            uint32_t rank = 0;
+            for (uint32_t f = 0; f < m; ++f) {
+                const double df = cd2[f];
+                rank += (df < de || (df == de && cidx[f] < ie)) ? 1u : 0u;
+            }
+            if (rank < need) {
+                const float4 p = C.xyz[ie];
+                cum_add(c, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
+            }
+        }
+        Cum t;
+        t.sx = lsm_wave_sum(c.sx);
+        t.sy = lsm_wave_sum(c.sy);
+        t.sz = lsm_wave_sum(c.sz);
+        t.sxx = lsm_wave_sum(c.sxx);
+        t.sxy = lsm_wave_sum(c.sxy);
+        t.sxz = lsm_wave_sum(c.sxz);
+        t.syy = lsm_wave_sum(c.syy);
+        t.syz = lsm_wave_sum(c.syz);
+        t.szz = lsm_wave_sum(c.szz);
+        int nn = c.n;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) nn += __shfl_xor(nn, off, LSM_WAVE);
+        t.n = nn;
+        if (lane == 0) {
+            float4 *nrm = const_cast<float4 *>(C.nrm);
+            nrm[j] = normal_from_cum(t);
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// download in reference order
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+download_kernel(const float4 *xyz, const float4 *nrm, const uint32_t *perm, int n, double *oxyz,
+                double *onrm) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t r = perm[j];
+    if (oxyz) {
+        float4 p = xyz[j];
+        oxyz[3 * r] = p.x;
+        oxyz[3 * r + 1] = p.y;
+        oxyz[3 * r + 2] = p.z;
+    }
+    if (onrm) {
+        float4 q = nrm[j];
+        onrm[3 * r] = q.x;
+        onrm[3 * r + 1] = q.y;
+        onrm[3 * r + 2] = q.z;
+    }
+}
+
+// helpers ----------------------------------------------------------------------------------
+template <typename T>
+int upload_vec(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out) {
+    T *d = static_cast<T *>(ctx->buf(name, v.size() * sizeof(T)));
+    if (!d) {
+        ctx->set_error(std::string("scratch allocation failed: ") + name);
+        return LSM_ENOMEM;
+    }
+    if (!v.empty())
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice,
+                                        ctx->stream));
+    *out = d;
+    return LSM_OK;
+}
+
+int ensure_cloud_buffers(lsm_ctx *ctx, Cloud *c, int64_t n, bool normals) {
+    if (c->cap < n || !c->d_xyz) {
+        (void)hipFree(c->d_xyz);
+        (void)hipFree(c->d_nrm);
+        (void)hipFree(c->d_perm);
+        c->d_xyz = nullptr;
+        c->d_nrm = nullptr;
+        c->d_perm = nullptr;
+        int64_t cap = std::max<int64_t>(n, 1);
+        if (hipMalloc(&c->d_xyz, cap * sizeof(float4)) != hipSuccess ||
+            hipMalloc(&c->d_perm, cap * sizeof(uint32_t)) != hipSuccess) {
+            ctx->set_error("hipMalloc failed for processed cloud");
+            return LSM_ENOMEM;
+        }
+        c->cap = cap;
+    }
+    if (normals && !c->d_nrm) {
+        if (hipMalloc(&c->d_nrm, c->cap * sizeof(float4)) != hipSuccess) {
+            ctx->set_error("hipMalloc failed for normals");
+            return LSM_ENOMEM;
+        }
+    }
+    return LSM_OK;
+}
+
+inline int bits_for(uint64_t v) {
+    int b = 1;
+    while (b < 64 && (uint64_t(1) << b) <= v) ++b;
+    return b;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// host orchestration
+// ==========================================================================================
+namespace {
+
+std::vector<Seg> point_segments(const std::vector<uint32_t> &n, int per_block) {
+    std::vector<Seg> segs;
+    for (size_t k = 0; k < n.size(); ++k)
+        for (uint32_t s = 0; s < n[k]; s += per_block) segs.push_back({int32_t(k), int32_t(s)});
+    return segs;
+}
+
+// filter_radius_height over the batch: writes the kept points of cloud k, in reference order, to
+// out[off[k] .. off[k] + cnt[k]).
+int run_filter(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params &p,
+               float4 **out, std::vector<uint32_t> &off, std::vector<uint32_t> &cnt) {
+    hipStream_t st = ctx->stream;
+    const int K = int(clouds.size());
+    std::vector<const float *> raw(K);
+    std::vector<int32_t> nraw(K), first_block(K), nblocks(K);
+    std::vector<Seg> fsegs;
+    int64_t total_raw = 0;
+    for (int k = 0; k < K; ++k) {
+        raw[k] = clouds[k]->d_raw;
+        nraw[k] = int32_t(clouds[k]->n_raw);
+        first_block[k] = int32_t(fsegs.size());
+        for (int64_t s = 0; s < clouds[k]->n_raw; s += FILTER_CHUNK)
+            fsegs.push_back({k, int32_t(s)});
+        nblocks[k] = int32_t(fsegs.size()) - first_block[k];
+        total_raw += clouds[k]->n_raw;
+    }
+    if (total_raw >= (int64_t(1) << 32)) {
+        ctx->set_error("batch too large (>= 2^32 raw points); split the batch");
+        return LSM_EINVAL;
+    }
+    const int nfb = int(fsegs.size());
+    int rc;
+    const float **d_raw;
+    int32_t *d_nraw;
+    Seg *d_fsegs;
+    if ((rc = upload_vec(ctx, "f_raw", raw, const_cast<const float ***>(&d_raw)))) return rc;
+    if ((rc = upload_vec(ctx, "f_nraw", nraw, &d_nraw))) return rc;
+    if ((rc = upload_vec(ctx, "f_segs", fsegs, &d_fsegs))) return rc;
+    uint32_t *d_bcount = (uint32_t *)ctx->buf("f_bcount", size_t(nfb + 1) * 4);
+    uint32_t *d_boff = (uint32_t *)ctx->buf("f_boff", size_t(nfb + 1) * 4);
+    float4 *d_fpts = (float4 *)ctx->buf("f_pts", size_t(std::max<int64_t>(total_raw, 1)) * 16);
+    uint32_t *d_fidx = (uint32_t *)ctx->buf("f_idx", size_t(std::max<int64_t>(total_raw, 1)) * 4);
+    if (!d_bcount || !d_boff || !d_fpts || !d_fidx) {
+        ctx->set_error("scratch allocation failed (filter)");
+        return LSM_ENOMEM;
+    }
+    FilterParams fp{p.max_radius * p.max_radius, p.min_radius * p.min_radius, p.min_height,
+                    p.max_height};
+    std::vector<uint32_t> boff_h(size_t(nfb) + 1, 0);
+    if (nfb > 0) {
+        hipEvent_t ev;
+        ctx->tic("filter", &ev);
+        filter_count<<<nfb, FILTER_THREADS, 0, st>>>(d_fsegs, d_raw, d_nraw, fp, d_bcount);
+        size_t tmpb = 0;
+        LSM_HIP_TRY(ctx, rocprim::exclusive_scan(nullptr, tmpb, d_bcount, d_boff, 0u, size_t(nfb) + 1,
+                                rocprim::plus<uint32_t>(), st));
+        void *tmp = ctx->buf("scan_tmp", tmpb);
+        // the extra element (bcount[nfb] = 0) turns boff[nfb] into the total
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_bcount + nfb, 0, 4, st));
+        LSM_HIP_TRY(ctx, rocprim::exclusive_scan(tmp, tmpb, d_bcount, d_boff, 0u, size_t(nfb) + 1,
+                                rocprim::plus<uint32_t>(), st));
+        filter_write<<<nfb, FILTER_THREADS, 0, st>>>(d_fsegs, d_raw, d_nraw, fp, d_boff, d_fpts,
+                                                     d_fidx);
+        ctx->toc("filter", ev);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(boff_h.data(), d_boff, boff_h.size() * 4,
+                                        hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    }
+    off.assign(K, 0);
+    cnt.assign(K, 0);
+    uint32_t run = 0;
+    for (int k = 0; k < K; ++k) {
+        if (nblocks[k] == 0) {
+            off[k] = run;
+            continue;
+        }
+        off[k] = boff_h[first_block[k]];
+        cnt[k] = boff_h[first_block[k] + nblocks[k]] - off[k];
+        run = off[k] + cnt[k];
+    }
+    *out = d_fpts;
+    return LSM_OK;
+}
+
+// voxel_down_sample over the batch; replaces (pts, off, cnt) by the voxel centroids (f32 working
+// copy) and stores the f64 centroids / int32 keys on each cloud.
+int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts,
+              std::vector<uint32_t> &off, std::vector<uint32_t> &cnt) {
+    hipStream_t st = ctx->stream;
+    const int K = int(clouds.size());
+    int rc;
+    uint32_t ntot = 0;
+    for (int k = 0; k < K; ++k) ntot = std::max(ntot, off[k] + cnt[k]);
+    uint32_t *d_off, *d_cnt;
+    if ((rc = upload_vec(ctx, "v_off", off, &d_off))) return rc;
+    if ((rc = upload_vec(ctx, "v_cnt", cnt, &d_cnt))) return rc;
+    double *d_bb = (double *)ctx->buf("v_bb", size_t(K) * 48);
+    if (!d_bb) return LSM_ENOMEM;
+    bbox_kernel<<<K, 256, 0, st>>>(*pts, d_off, d_cnt, d_bb);
+    std::vector<double> bb(size_t(K) * 6);
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(bb.data(), d_bb, bb.size() * 8, hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    std::vector<VoxGeo> geo(K);
+    uint64_t key_off = 0;
+    for (int k = 0; k < K; ++k) {
+        VoxGeo &G = geo[k];
+        G = {0.0, 0.0, 0.0, 1, 1, 1, key_off};
+        if (cnt[k] == 0) continue;
+        // Open3D: voxel_min_bound = min_bound - v3 * 0.5; voxel_max_bound = max_bound + v3 * 0.5
+        const double half = v * 0.5;
+        double vmin[3], vmax[3];
+        for (int a = 0; a < 3; ++a) {
+            vmin[a] = bb[6 * k + a] - half;
+            vmax[a] = bb[6 * k + 3 + a] + half;
+        }
+        const double ext =
+            std::max(vmax[0] - vmin[0], std::max(vmax[1] - vmin[1], vmax[2] - vmin[2]));
+        if (v * double(std::numeric_limits<int>::max()) < ext) {
+            ctx->set_error("voxel_size is too small.");
+            return LSM_EINVAL;
+        }
+        int64_t d[3];
+        for (int a = 0; a < 3; ++a)
+            d[a] = (int64_t)std::floor((bb[6 * k + 3 + a] - vmin[a]) / v) + 2;
+        const uint64_t cells = uint64_t(d[0]) * uint64_t(d[1]) * uint64_t(d[2]);
+        if (cells > (uint64_t(1) << 44)) {
+            ctx->set_error("voxel grid too large for the 64-bit key space");
+            return LSM_EINVAL;
+        }
+        G = {vmin[0], vmin[1], vmin[2], d[0], d[1], d[2], key_off};
+        key_off += cells;
+    }
+    VoxGeo *d_geo;
+    if ((rc = upload_vec(ctx, "v_geo", geo, &d_geo))) return rc;
+    std::vector<Seg> segs = point_segments(cnt, PT_THREADS);
+    Seg *d_segs;
+    if ((rc = upload_vec(ctx, "v_segs", segs, &d_segs))) return rc;
+    const size_t N = std::max<uint32_t>(ntot, 1);
+    uint64_t *k_in = (uint64_t *)ctx->buf("v_kin", N * 8);
+    uint64_t *k_out = (uint64_t *)ctx->buf("v_kout", N * 8);
+    uint32_t *v_in = (uint32_t *)ctx->buf("v_vin", N * 4);
+    uint32_t *v_out = (uint32_t *)ctx->buf("v_vout", N * 4);
+    uint32_t *flag = (uint32_t *)ctx->buf("v_flag", N * 4 + 4);
+    uint32_t *vid = (uint32_t *)ctx->buf("v_vid", N * 4 + 4);
+    int32_t *ptc = (int32_t *)ctx->buf("v_ptc", N * 4);
+    double *cent = (double *)ctx->buf("v_cent", N * 24);
+    int32_t *vkeys = (int32_t *)ctx->buf("v_keys", N * 12);
+    float4 *vpts = (float4 *)ctx->buf("v_pts", N * 16);
+    int32_t *vcloud = (int32_t *)ctx->buf("v_vcloud", N * 4);
+    if (!k_in || !k_out || !v_in || !v_out || !flag || !vid || !ptc || !cent || !vkeys || !vpts ||
+        !vcloud) {
+        ctx->set_error("scratch allocation failed (voxel)");
+        return LSM_ENOMEM;
+    }
+    uint32_t nvox = 0;
+    std::vector<uint32_t> vcount(K, 0);
+    if (!segs.empty()) {
+        hipEvent_t ev;
+        ctx->tic("voxel", &ev);
+        voxel_keys<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, *pts, d_off, d_cnt, d_geo, v,
+                                                           k_in, v_in);
+        point_cloud_ids<<<dim3(64, K), 256, 0, st>>>(d_off, d_cnt, K, ptc);
+        const int endbit = bits_for(key_off);
+        size_t tmpb = 0;
+        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(nullptr, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit,
+                                  st));
+        void *tmp = ctx->buf("sort_tmp", tmpb);
+        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(tmp, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit, st));
+        const int nb = int((ntot + PT_THREADS - 1) / PT_THREADS);
+        voxel_flags<<<nb, PT_THREADS, 0, st>>>(k_out, ntot, flag);
+        LSM_HIP_TRY(ctx, hipMemsetAsync(flag + ntot, 0, 4, st));
+        tmpb = 0;
+        LSM_HIP_TRY(ctx, rocprim::exclusive_scan(nullptr, tmpb, flag, vid, 0u, size_t(ntot) + 1,
+                                rocprim::plus<uint32_t>(), st));
+        tmp = ctx->buf("scan_tmp", tmpb);
+        LSM_HIP_TRY(ctx, rocprim::exclusive_scan(tmp, tmpb, flag, vid, 0u, size_t(ntot) + 1,
+                                rocprim::plus<uint32_t>(), st));
+        voxel_reduce<<<nb, PT_THREADS, 0, st>>>(k_out, v_out, vid, flag, ntot, *pts, ptc, d_geo,
+                                                cent, vkeys, vpts, vcloud);
+        ctx->toc("voxel", ev);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(&nvox, vid + ntot, 4, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        std::vector<int32_t> vc(nvox);
+        if (nvox) {
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(vc.data(), vcloud, size_t(nvox) * 4,
+                                            hipMemcpyDeviceToHost, st));
+            LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        }
+        for (uint32_t i = 0; i < nvox; ++i) vcount[vc[i]]++;
+    }
+    uint32_t run = 0;
+    for (int k = 0; k < K; ++k) {
+        off[k] = run;
+        cnt[k] = vcount[k];
+        run += vcount[k];
+    }
+    for (int k = 0; k < K; ++k) {
+        Cloud *c = clouds[k];
+        if (c->vox_cap < int64_t(cnt[k]) || !c->d_vox) {
+            (void)hipFree(c->d_vox);
+            (void)hipFree(c->d_vkeys);
+            c->d_vox = nullptr;
+            c->d_vkeys = nullptr;
+            c->vox_cap = std::max<int64_t>(cnt[k], 1);
+            if (hipMalloc(&c->d_vox, c->vox_cap * 24) != hipSuccess ||
+                hipMalloc(&c->d_vkeys, c->vox_cap * 12) != hipSuccess) {
+                ctx->set_error("hipMalloc failed (voxel outputs)");
+                return LSM_ENOMEM;
+            }
+        }
+        if (cnt[k]) {
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_vox, cent + size_t(off[k]) * 3, size_t(cnt[k]) * 24,
+                                            hipMemcpyDeviceToDevice, st));
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_vkeys, vkeys + size_t(off[k]) * 3,
+                                            size_t(cnt[k]) * 12, hipMemcpyDeviceToDevice, st));
+        }
+    }
+    *pts = vpts;
+    return LSM_OK;
+}
+
+}  // namespace
+
+int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params &p,
+                   int64_t *n_out) {
+    hipStream_t st = ctx->stream;
+    const int K = int(clouds.size());
+    int rc;
+    hipEvent_t ev;
+
+    // ---------------- filter / voxel ----------------
+    float4 *wpts = nullptr;
+    std::vector<uint32_t> woff, wn;
+    if ((rc = run_filter(ctx, clouds, p, &wpts, woff, wn))) return rc;
+    const bool vox = p.voxel_size > 0.0;
+    if (vox && (rc = run_voxel(ctx, clouds, p.voxel_size, &wpts, woff, wn))) return rc;
+
+    // ---------------- spatial grid ----------------
+    uint32_t *d_coff, *d_cn;
+    if ((rc = upload_vec(ctx, "g_off", woff, &d_coff))) return rc;
+    if ((rc = upload_vec(ctx, "g_cnt", wn, &d_cn))) return rc;
+    double *d_bb = (double *)ctx->buf("g_bb", size_t(K) * 48);
+    if (!d_bb) return LSM_ENOMEM;
+    bbox_kernel<<<K, 256, 0, st>>>(wpts, d_coff, d_cn, d_bb);
+    std::vector<double> bb(size_t(K) * 6);
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(bb.data(), d_bb, bb.size() * 8, hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+
+    std::vector<GridGeo> geo(K);
+    uint64_t cell_total = 0;
+    const float cell_req = p.grid_cell > 0 ? float(p.grid_cell) : 0.3f;
+    for (int k = 0; k < K; ++k) {
+        GridGeo &G = geo[k];
+        G.pt_off = woff[k];
+        G.n = wn[k];
+        G.pad = 0;
+        G.ox = G.oy = G.oz = 0.f;
+        G.nx = G.ny = G.nz = 1;
+        float c = cell_req;
+        if (wn[k] > 0) {
+            float ext[3];
+            for (int a = 0; a < 3; ++a) ext[a] = float(bb[6 * k + 3 + a] - bb[6 * k + a]);
+            for (;;) {
+                const int64_t nx = int64_t(std::floor(ext[0] / c)) + 1;
+                const int64_t ny = int64_t(std::floor(ext[1] / c)) + 1;
+                const int64_t nz = int64_t(std::floor(ext[2] / c)) + 1;
+                if (nx * ny * nz <= MAX_CELLS_PER_CLOUD) {
+                    G.nx = int(nx);
+                    G.ny = int(ny);
+                    G.nz = int(nz);
+                    break;
+                }
+                c *= 1.25f;
+            }
+            G.ox = float(bb[6 * k]);
+            G.oy = float(bb[6 * k + 1]);
+            G.oz = float(bb[6 * k + 2]);
+        }
+        G.cell = c;
+        G.inv_cell = 1.f / c;
+        G.cell_off = uint32_t(cell_total);
+        cell_total += uint64_t(G.nx) * G.ny * G.nz;
+        if (cell_total >= (uint64_t(1) << 32) - 1) {
+            ctx->set_error("batch too large for the 32-bit cell key space; split the batch");
+            return LSM_EINVAL;
+        }
+    }
+    std::vector<CloudDev> cdev(K);
+    std::vector<uint32_t *> perm_ptrs(K), cell_ptrs(K);
+    for (int k = 0; k < K; ++k) {
+        Cloud *c = clouds[k];
+        if ((rc = ensure_cloud_buffers(ctx, c, wn[k], p.want_normals != 0))) return rc;
+        const int64_t ncells = int64_t(geo[k].nx) * geo[k].ny * geo[k].nz;
+        if (c->cell_cap < ncells + 1 || !c->d_cell) {
+            (void)hipFree(c->d_cell);
+            c->d_cell = nullptr;
+            c->cell_cap = ncells + 1;
+            if (hipMalloc(&c->d_cell, size_t(c->cell_cap) * 4) != hipSuccess) {
+                ctx->set_error("hipMalloc failed (cell table)");
+                return LSM_ENOMEM;
+            }
+        }
+        CloudDev &D = cdev[k];
+        D.xyz = c->d_xyz;
+        D.nrm = p.want_normals ? c->d_nrm : nullptr;
+        D.cell_start = c->d_cell;
+        D.ox = geo[k].ox;
+        D.oy = geo[k].oy;
+        D.oz = geo[k].oz;
+        D.cell = geo[k].cell;
+        D.inv_cell = geo[k].inv_cell;
+        D.nx = geo[k].nx;
+        D.ny = geo[k].ny;
+        D.nz = geo[k].nz;
+        D.n = int(wn[k]);
+        perm_ptrs[k] = c->d_perm;
+        cell_ptrs[k] = c->d_cell;
+    }
+    GridGeo *d_geo;
+    CloudDev *d_cd;
+    uint32_t **d_perm_ptrs, **d_cell_ptrs;
+    if ((rc = upload_vec(ctx, "g_geo", geo, &d_geo))) return rc;
+    if ((rc = upload_vec(ctx, "g_cd", cdev, &d_cd))) return rc;
+    if ((rc = upload_vec(ctx, "g_perm", perm_ptrs, &d_perm_ptrs))) return rc;
+    if ((rc = upload_vec(ctx, "g_cellp", cell_ptrs, &d_cell_ptrs))) return rc;
+    std::vector<Seg> psegs = point_segments(wn, PT_THREADS);
+    Seg *d_psegs;
+    if ((rc = upload_vec(ctx, "g_segs", psegs, &d_psegs))) return rc;
+    uint32_t ntot = 0;
+    for (int k = 0; k < K; ++k) ntot = std::max(ntot, woff[k] + wn[k]);
+    const size_t N = std::max<uint32_t>(ntot, 1);
+    uint32_t *k_in = (uint32_t *)ctx->buf("g_kin", N * 4);
+    uint32_t *k_out = (uint32_t *)ctx->buf("g_kout", N * 4);
+    uint32_t *v_in = (uint32_t *)ctx->buf("g_vin", N * 4);
+    uint32_t *v_out = (uint32_t *)ctx->buf("g_vout", N * 4);
+    uint32_t *nonempty = (uint32_t *)ctx->buf("g_nonempty", size_t(K) * 4);
+    if (!k_in || !k_out || !v_in || !v_out || !nonempty) {
+        ctx->set_error("scratch allocation failed (grid)");
+        return LSM_ENOMEM;
+    }
+    ctx->tic("grid", &ev);
+    LSM_HIP_TRY(ctx, hipMemsetAsync(nonempty, 0, size_t(K) * 4, st));
+    if (!psegs.empty()) {
+        grid_keys<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, wpts, d_geo, k_in, v_in);
+        size_t tmpb = 0;
+        const int endbit = bits_for(cell_total);
+        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(nullptr, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit,
+                                  st));
+        void *tmp = ctx->buf("sort_tmp", tmpb);
+        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(tmp, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit, st));
+        grid_scatter<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_geo, d_cd, v_out, k_out,
+                                                              wpts, d_perm_ptrs, nonempty);
+    }
+    {
+        int64_t maxcells = 0;
+        for (int k = 0; k < K; ++k)
+            maxcells = std::max<int64_t>(maxcells, int64_t(geo[k].nx) * geo[k].ny * geo[k].nz + 1);
+        const int64_t chunks = (maxcells + FILL_CHUNK - 1) / FILL_CHUNK;
+        const int gx = int(std::min<int64_t>((chunks + 255) / 256, 1024));
+        grid_fill<<<dim3(gx, K), 256, 0, st>>>(d_geo, K, k_out, d_cell_ptrs);
+    }
+    ctx->toc("grid", ev);
+
+    // ---------------- normals ----------------
+    if (p.want_normals && !psegs.empty()) {
+        NormalParams np;
+        np.r2 = p.normal_radius * p.normal_radius;
+        np.r = float(p.normal_radius);
+        np.max_nn = p.max_nn;
+        const uint32_t cap = std::max<uint32_t>(ntot, 1);
+        uint32_t *ov = (uint32_t *)ctx->buf("n_ov", size_t(cap) * 8);
+        uint32_t *ovn = (uint32_t *)ctx->buf("n_ovn", 16);
+        if (!ov || !ovn) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, hipMemsetAsync(ovn, 0, 4, st));
+        ctx->tic("normals", &ev);
+        normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, ov, ovn, cap);
+        ctx->toc("normals", ev);
+        ctx->tic("normals_overflow", &ev);
+        normals_overflow<<<8192, LSM_WAVE, 0, st>>>(d_cd, np, ov, ovn, cap);
+        ctx->toc("normals_overflow", ev);
+    }
+
+    std::vector<uint32_t> hne(K);
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(hne.data(), nonempty, size_t(K) * 4, hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    LSM_HIP_TRY(ctx, hipGetLastError());
+    ctx->collect_timings();
+    for (int k = 0; k < K; ++k) {
+        Cloud *c = clouds[k];
+        c->n = wn[k];
+        c->processed = true;
+        c->has_normals = p.want_normals != 0;
+        c->voxelized = vox;
+        c->dev = cdev[k];
+        c->nonempty_cells = hne[k];
+        if (n_out) n_out[k] = wn[k];
+    }
+    return LSM_OK;
+}
+
+int lsm_download_run(lsm_ctx *ctx, Cloud *c, double *xyz, double *nrm, int64_t cap) {
+    (void)cap;
+    hipStream_t st = ctx->stream;
+    const int n = int(c->n);
+    if (n == 0) return LSM_OK;
+    double *dx = (double *)ctx->buf("dl_xyz", size_t(n) * 24);
+    double *dn = (double *)ctx->buf("dl_nrm", size_t(n) * 24);
+    if (!dx || !dn) return LSM_ENOMEM;
+    const bool xyz_from_vox = c->voxelized;
+    download_kernel<<<(n + 255) / 256, 256, 0, st>>>(c->d_xyz, c->d_nrm, c->d_perm, n,
+                                                     (xyz && !xyz_from_vox) ? dx : nullptr,
+                                                     nrm ? dn : nullptr);
+    if (xyz) {
+        if (xyz_from_vox)
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(xyz, c->d_vox, size_t(n) * 24, hipMemcpyDeviceToHost, st));
+        else
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(xyz, dx, size_t(n) * 24, hipMemcpyDeviceToHost, st));
+    }
+    if (nrm) LSM_HIP_TRY(ctx, hipMemcpyAsync(nrm, dn, size_t(n) * 24, hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    return LSM_OK;
+}

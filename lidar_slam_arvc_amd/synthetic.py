@@ -1,0 +1,276 @@
+"""Seeded synthetic LiDAR scenes for tests and the benchmark.
+
+The reference ships no data (its datasets live under absolute paths, run_scanmatcher.py:146-157),
+so every workload here is synthetic, as SURVEY.md §8d specifies:
+
+* a ground plane at world z = 0 seen from a sensor mounted 0.69 m above it (the reference's
+  ground-plane model ``[0, 0, 1, 0.69]``, keyframe.py:436);
+* axis-aligned boxes (buildings, parked objects), thin wall segments and vertical poles placed
+  in a band around a closed trajectory;
+* a spinning multi-ring LiDAR (HDL-64 / Ouster-128 / 16-ring) ray-cast against that scene,
+  range noise N(0, 0.02 m), returns beyond 60 m dropped.
+
+Scans come out as float32 N x 3 arrays in the sensor frame, ring-major (all azimuths of ring 0,
+then ring 1, ...), misses removed -- the same shape ``o3d.io.read_point_cloud`` hands the
+reference (keyframe.py:45). Poses are 4x4 float64 world<-sensor transforms.
+
+This module is data generation only; it is not part of the registration path.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+SENSOR_HEIGHT = 0.69
+
+
+@dataclass(frozen=True)
+class LidarModel:
+    rings: int
+    azimuths: int
+    el_min_deg: float
+    el_max_deg: float
+    max_range: float = 60.0
+    noise: float = 0.02
+
+    def directions(self) -> np.ndarray:
+        el = np.deg2rad(np.linspace(self.el_min_deg, self.el_max_deg, self.rings))
+        az = np.arange(self.azimuths) * (2.0 * np.pi / self.azimuths)
+        ce, se = np.cos(el)[:, None], np.sin(el)[:, None]
+        d = np.stack([ce * np.cos(az)[None, :], ce * np.sin(az)[None, :],
+                      np.broadcast_to(se, (self.rings, self.azimuths))], axis=-1)
+        return d.reshape(-1, 3)
+
+
+VLP16_8K = LidarModel(16, 512, -15.0, 15.0)          # C1: 8,192 rays
+HDL64 = LidarModel(64, 1024, -24.9, 2.0)             # C2/C3/C4: 65,536 rays
+OUSTER128 = LidarModel(128, 2048, -22.5, 22.5)       # C5: 262,144 rays
+
+
+@dataclass
+class Scene:
+    boxes: np.ndarray                 # K x 6 (xmin, ymin, zmin, xmax, ymax, zmax)
+    poles: np.ndarray                 # P x 4 (cx, cy, radius, height)
+    path: np.ndarray = field(default_factory=lambda: np.zeros((0, 2)))
+
+
+def loop_path(length_m: float = 1000.0, n: int = 4000) -> np.ndarray:
+    """Closed, gently wavy loop of the given length (x, y samples, uniform in arc length)."""
+    th = np.linspace(0.0, 2.0 * np.pi, 8 * n, endpoint=False)
+    r = 1.0 + 0.12 * np.sin(3 * th) + 0.05 * np.cos(5 * th)
+    xy = np.stack([r * np.cos(th), r * np.sin(th)], axis=1)
+    seg = np.linalg.norm(np.diff(np.vstack([xy, xy[:1]]), axis=0), axis=1)
+    xy *= length_m / seg.sum()
+    s = np.concatenate([[0.0], np.cumsum(seg * length_m / seg.sum())])[:-1]
+    su = np.linspace(0.0, length_m, n, endpoint=False)
+    return np.stack([np.interp(su, s, xy[:, 0]), np.interp(su, s, xy[:, 1])], axis=1)
+
+
+def make_scene(seed: int, path: np.ndarray) -> Scene:
+    """Objects in a band around ``path``: boxes, wall segments and poles, never on the path."""
+    rng = np.random.default_rng(seed)
+    seg = np.diff(np.vstack([path, path[:1]]), axis=0)
+    s = np.concatenate([[0.0], np.cumsum(np.linalg.norm(seg, axis=1))])
+    total = s[-1]
+
+    def frame_at(u):
+        x = np.interp(u % total, s[:-1], path[:, 0])
+        y = np.interp(u % total, s[:-1], path[:, 1])
+        x2 = np.interp((u + 1.0) % total, s[:-1], path[:, 0])
+        y2 = np.interp((u + 1.0) % total, s[:-1], path[:, 1])
+        t = np.array([x2 - x, y2 - y])
+        t /= max(np.linalg.norm(t), 1e-9)
+        return np.array([x, y]), t, np.array([-t[1], t[0]])
+
+    boxes, poles = [], []
+    for u in np.arange(0.0, total, 4.0):
+        p, t, nrm = frame_at(u + rng.uniform(0, 5))
+        for side in (-1.0, 1.0):
+            if rng.random() < 0.8:       # building / object box
+                off = side * rng.uniform(4.0, 22.0)
+                c = p + off * nrm
+                hx, hy = rng.uniform(0.25, 1.5, size=2)
+                h = rng.uniform(0.5, 8.0)
+                boxes.append([c[0] - hx, c[1] - hy, 0.0, c[0] + hx, c[1] + hy, h])
+            if rng.random() < 0.45:      # pole
+                off = side * rng.uniform(3.0, 12.0)
+                c = p + off * nrm
+                poles.append([c[0], c[1], rng.uniform(0.1, 0.3), rng.uniform(2.0, 7.0)])
+            if rng.random() < 0.5:       # wall segment, axis aligned, 15-25 m out
+                off = side * rng.uniform(15.0, 25.0)
+                c = p + off * nrm
+                ln = rng.uniform(4.0, 10.0)
+                if abs(t[0]) > abs(t[1]):
+                    boxes.append([c[0] - ln / 2, c[1] - 0.15, 0.0, c[0] + ln / 2, c[1] + 0.15,
+                                  rng.uniform(2.0, 4.0)])
+                else:
+                    boxes.append([c[0] - 0.15, c[1] - ln / 2, 0.0, c[0] + 0.15, c[1] + ln / 2,
+                                  rng.uniform(2.0, 4.0)])
+    return Scene(np.asarray(boxes, dtype=np.float64).reshape(-1, 6),
+                 np.asarray(poles, dtype=np.float64).reshape(-1, 4), path)
+
+
+def path_pose(path: np.ndarray, u: float, rng: np.random.Generator | None = None,
+              tilt_deg: float = 0.5) -> np.ndarray:
+    """World<-sensor pose at arc length ``u`` along ``path`` (yaw along the tangent)."""
+    seg = np.diff(np.vstack([path, path[:1]]), axis=0)
+    s = np.concatenate([[0.0], np.cumsum(np.linalg.norm(seg, axis=1))])
+    total = s[-1]
+    x = np.interp(u % total, s[:-1], path[:, 0])
+    y = np.interp(u % total, s[:-1], path[:, 1])
+    x2 = np.interp((u + 0.5) % total, s[:-1], path[:, 0])
+    y2 = np.interp((u + 0.5) % total, s[:-1], path[:, 1])
+    yaw = math.atan2(y2 - y, x2 - x)
+    roll = pitch = 0.0
+    if rng is not None:
+        roll, pitch = np.deg2rad(rng.normal(0.0, tilt_deg, size=2))
+    return pose_from(x, y, SENSOR_HEIGHT, roll, pitch, yaw)
+
+
+def rot_xyz(roll: float, pitch: float, yaw: float) -> np.ndarray:
+    cr, sr, cp, sp, cy, sy = (math.cos(roll), math.sin(roll), math.cos(pitch), math.sin(pitch),
+                              math.cos(yaw), math.sin(yaw))
+    rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1.0]])
+    ry = np.array([[cp, 0, sp], [0, 1.0, 0], [-sp, 0, cp]])
+    rx = np.array([[1.0, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    return rz @ ry @ rx
+
+
+def pose_from(x, y, z, roll, pitch, yaw) -> np.ndarray:
+    T = np.eye(4)
+    T[:3, :3] = rot_xyz(roll, pitch, yaw)
+    T[:3, 3] = (x, y, z)
+    return T
+
+
+def perturb(T: np.ndarray, rng: np.random.Generator, sigma_t: float, sigma_rot_deg: float,
+            yaw_only: bool = False) -> np.ndarray:
+    """T composed with a small random motion (odometry-like prior)."""
+    r = np.deg2rad(rng.normal(0.0, sigma_rot_deg, size=3))
+    if yaw_only:
+        r[:2] = 0.0
+    D = pose_from(*rng.normal(0.0, sigma_t, size=3), *r)
+    return T @ D
+
+
+def raycast(scene: Scene, pose: np.ndarray, model: LidarModel, rng: np.random.Generator,
+            chunk: int = 16384) -> np.ndarray:
+    """Ray-cast one spinning scan; returns float32 M x 3 sensor-frame points (misses removed)."""
+    d_s = model.directions()
+    R, o = pose[:3, :3], pose[:3, 3]
+    d_w = d_s @ R.T
+    near = model.max_range + 3.0
+    bx = scene.boxes
+    if len(bx):
+        cx = np.clip(o[0], bx[:, 0], bx[:, 3]) - o[0]
+        cy = np.clip(o[1], bx[:, 1], bx[:, 4]) - o[1]
+        bx = bx[cx * cx + cy * cy < near * near]
+    pl = scene.poles
+    if len(pl):
+        pl = pl[(pl[:, 0] - o[0]) ** 2 + (pl[:, 1] - o[1]) ** 2 < near * near]
+    t_hit = np.full(len(d_w), np.inf)
+    for a in range(0, len(d_w), chunk):
+        d = d_w[a:a + chunk]
+        best = np.full(len(d), np.inf)
+        dz = d[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            tg = np.where(dz < -1e-9, -o[2] / dz, np.inf)
+        best = np.minimum(best, tg)
+        if len(bx):
+            with np.errstate(divide="ignore", invalid="ignore"):
+                inv = 1.0 / d
+                t1 = (bx[None, :, 0:3] - o[None, None, :]) * inv[:, None, :]
+                t2 = (bx[None, :, 3:6] - o[None, None, :]) * inv[:, None, :]
+            tmin = np.nanmax(np.minimum(t1, t2), axis=2)
+            tmax = np.nanmin(np.maximum(t1, t2), axis=2)
+            ok = (tmax >= np.maximum(tmin, 1e-6))
+            tb = np.where(ok, np.where(tmin > 1e-6, tmin, np.inf), np.inf)
+            best = np.minimum(best, tb.min(axis=1))
+        if len(pl):
+            ox = o[0] - pl[None, :, 0]
+            oy = o[1] - pl[None, :, 1]
+            a2 = (d[:, 0:1] ** 2 + d[:, 1:2] ** 2)
+            b2 = 2.0 * (ox * d[:, 0:1] + oy * d[:, 1:2])
+            c2 = ox * ox + oy * oy - pl[None, :, 2] ** 2
+            disc = b2 * b2 - 4.0 * a2 * c2
+            with np.errstate(divide="ignore", invalid="ignore"):
+                tc = (-b2 - np.sqrt(np.maximum(disc, 0.0))) / (2.0 * a2)
+            z = o[2] + tc * d[:, 2:3]
+            okc = (disc > 0) & (tc > 1e-6) & (z >= 0.0) & (z <= pl[None, :, 3])
+            best = np.minimum(best, np.where(okc, tc, np.inf).min(axis=1))
+        t_hit[a:a + chunk] = best
+    hit = np.isfinite(t_hit) & (t_hit <= model.max_range)
+    rng_noise = rng.normal(0.0, model.noise, size=len(d_s))
+    t = t_hit + rng_noise
+    pts = d_s[hit] * t[hit, None]
+    return pts.astype(np.float32)
+
+
+@dataclass
+class Sequence:
+    """Keyframes along a path: scans, ground-truth poses, odometry-like relative priors."""
+    scans: list
+    poses: np.ndarray          # K x 4 x 4 world<-sensor (ground truth)
+    priors: np.ndarray         # (K-1) x 4 x 4 noisy relative transforms T_i^-1 T_{i+1}
+
+
+def make_sequence(n_keyframes: int, seed: int = 3, model: LidarModel = HDL64,
+                  spacing: float = 0.5, start: float = 0.0, path_length: float = 1000.0,
+                  sigma_t: float = 0.05, sigma_rot_deg: float = 1.0,
+                  first_index: int = 0) -> Sequence:
+    """C3-style sequence: keyframes every ``spacing`` metres along a closed loop.
+
+    ``first_index`` lets ranks generate disjoint chunks of one global sequence: keyframe ``k``
+    always gets the same pose, scan noise and prior no matter which chunk generates it.
+    """
+    path = loop_path(path_length)
+    scene = make_scene(seed, path)
+    scans, poses = [], []
+    for k in range(first_index, first_index + n_keyframes):
+        rng = np.random.default_rng([seed, k])
+        T = path_pose(path, start + k * spacing, rng)
+        poses.append(T)
+        scans.append(raycast(scene, T, model, rng))
+    poses = np.asarray(poses)
+    priors = []
+    for k in range(first_index, first_index + n_keyframes - 1):
+        rng = np.random.default_rng([seed, k, 7])
+        j = k - first_index
+        rel = np.linalg.inv(poses[j]) @ poses[j + 1]
+        priors.append(perturb(rel, rng, sigma_t, sigma_rot_deg))
+    return Sequence(scans, poses, np.asarray(priors).reshape(-1, 4, 4))
+
+
+@dataclass
+class PairSet:
+    """Independent revisit pairs (C4 loop-closure batch)."""
+    targets: list
+    sources: list
+    gt: np.ndarray             # P x 4 x 4, T_target^-1 T_source
+    init: np.ndarray           # P x 4 x 4 noisy initial guesses
+
+
+def make_revisit_pairs(n_pairs: int, seed: int = 4, model: LidarModel = HDL64,
+                       path_length: float = 1000.0, sigma_t: float = 0.3,
+                       sigma_yaw_deg: float = 3.0, first_index: int = 0) -> PairSet:
+    """C4-style pairs: a pose on the loop and a revisit 0.5-2 m / <=10 deg away."""
+    path = loop_path(path_length)
+    scene = make_scene(seed, path)
+    tg, sc, gt, init = [], [], [], []
+    for k in range(first_index, first_index + n_pairs):
+        rng = np.random.default_rng([seed, k])
+        u = rng.uniform(0.0, path_length)
+        Ti = path_pose(path, u, rng)
+        off = rng.uniform(0.5, 2.0)
+        ang = rng.uniform(0, 2 * np.pi)
+        D = pose_from(off * math.cos(ang), off * math.sin(ang), 0.0, 0.0, 0.0,
+                      np.deg2rad(rng.uniform(-10.0, 10.0)))
+        Tj = Ti @ D
+        tg.append(raycast(scene, Ti, model, rng))
+        sc.append(raycast(scene, Tj, model, rng))
+        rel = np.linalg.inv(Ti) @ Tj
+        gt.append(rel)
+        init.append(perturb(rel, rng, sigma_t, sigma_yaw_deg, yaw_only=True))
+    return PairSet(tg, sc, np.asarray(gt), np.asarray(init))

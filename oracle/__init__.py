@@ -1,0 +1,15 @@
+"""CPU oracle for the ICP scan-matching hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``bench.py`` may
+import this package, and only as the checker / the timed CPU baseline. The product path
+(``lidar_slam_arvc_amd``) never imports it and never falls back to it.
+
+Pinning status:
+* filter, loop-closure candidate search, SE(3) host math: pinned bit-exactly against golden
+  vectors captured by importing the reference modules in the build container
+  (``tests/golden/make_golden.py``).
+* voxel down-sample, hybrid-kNN normals, ICP (P2P / P2Plane): the arithmetic lives in Open3D, which
+  is un-vendored and absent here, so these are *parity unpinned* by reference
+  fixtures. They are restated from Open3D's published algorithm and pinned by known-answer tests
+  (recovery of known transforms, exact Umeyama, planar normals, hand-computed voxel keys).
+"""

@@ -1,0 +1,481 @@
+"""Float64 NumPy/SciPy restatement of the reference's hot path -- TEST INFRASTRUCTURE ONLY.
+
+Not part of the product: only tests, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline
+leg use it, as the checker. See ``oracle/__init__.py`` for the pinning status.
+
+Every function cites the reference call site it restates. Where the arithmetic sits inside
+Open3D (un-vendored, unpinned: requirements.txt:2), the docstring names the Open3D operator
+([O3D]) and the published algorithm it follows (Open3D >= 0.15, nanoflann-backed KDTreeFlann).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+from scipy.spatial import cKDTree
+
+# ICP_PARAMETERS defaults (config/icp_parameters.yaml:1-22 via config/config.py:28-51) and the
+# hard-coded normal radius (keyframe.py:33).
+MIN_RADIUS, MAX_RADIUS = 0.5, 35
+MIN_HEIGHT, MAX_HEIGHT = -1.0, 50.0
+NORMAL_RADIUS, MAX_NN = 0.3, 300
+DISTANCE_THRESHOLD = 10.0
+
+
+# --------------------------------------------------------------------------------------------
+# a2: KeyFrame.filter_radius_height  (keyframe.py:74-94)
+# --------------------------------------------------------------------------------------------
+def filter_radius_height(points, min_radius=MIN_RADIUS, max_radius=MAX_RADIUS,
+                         min_height=MIN_HEIGHT, max_height=MAX_HEIGHT):
+    """Order-preserving strict radius/height mask in float64 (keyframe.py:88-93)."""
+    p = np.asarray(points, dtype=np.float64)
+    x, y, z = p[:, 0], p[:, 1], p[:, 2]
+    r2 = x ** 2 + y ** 2
+    keep = (r2 < max_radius ** 2) & (r2 > min_radius ** 2) & (z > min_height) & (z < max_height)
+    return p[np.where(keep)]
+
+
+# --------------------------------------------------------------------------------------------
+# a3: PointCloud.voxel_down_sample  (keyframe.py:108-111, :150-151)  [O3D VoxelDownSample]
+# --------------------------------------------------------------------------------------------
+INT_MAX = 2147483647
+
+
+def voxel_down_sample(points, voxel_size):
+    """Open3D VoxelDownSample: min_bound - v/2 origin, floor((p - o) / v) keys, per-voxel mean.
+
+    Returns (keys K x 3 int64, centroids K x 3 float64) sorted lexicographically by key
+    (Open3D's own output order is unordered_map iteration order, i.e. unspecified). Sums run in
+    point-index order, as Open3D's AccumulatedPoint does, so centroids are bit-reproducible.
+    """
+    p = np.asarray(points, dtype=np.float64)
+    if voxel_size <= 0.0:
+        raise RuntimeError("voxel_size <= 0.")
+    if len(p) == 0:
+        return np.zeros((0, 3), np.int64), np.zeros((0, 3))
+    vmin = p.min(axis=0) - voxel_size * 0.5
+    vmax = p.max(axis=0) + voxel_size * 0.5
+    if voxel_size * INT_MAX < (vmax - vmin).max():
+        raise RuntimeError("voxel_size is too small.")
+    keys = np.floor((p - vmin) / voxel_size).astype(np.int64)
+    order = np.lexsort((keys[:, 2], keys[:, 1], keys[:, 0]))     # stable: index order inside
+    ks = keys[order]
+    brk = np.ones(len(ks), dtype=bool)
+    brk[1:] = np.any(ks[1:] != ks[:-1], axis=1)
+    starts = np.flatnonzero(brk)
+    ends = np.append(starts[1:], len(ks))
+    cent = np.empty((len(starts), 3))
+    ps = p[order]
+    for v, (a, b) in enumerate(zip(starts, ends)):
+        acc = np.zeros(3)
+        for i in range(a, b):                 # sequential, index order (AccumulatedPoint::AddPoint)
+            acc = acc + ps[i]
+        cent[v] = acc / float(b - a)
+    return ks[starts], cent
+
+
+# --------------------------------------------------------------------------------------------
+# a4: PointCloud.estimate_normals(KDTreeSearchParamHybrid(0.3, 300))  (keyframe.py:160-162)
+#     [O3D EstimateNormals -> EstimatePerPointCovariances -> ComputeCovariance -> FastEigen3x3]
+# --------------------------------------------------------------------------------------------
+def sq_dist(q, p):
+    """nanoflann L2_Adaptor::evalMetric for dim 3: ((0 + dx^2) + dy^2) + dz^2, dx = q - p."""
+    d = q - p
+    return (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+
+
+def hybrid_search(tree, points, queries, radius, max_nn):
+    """KDTreeFlann::SearchHybrid: the max_nn nearest, truncated to d^2 < radius^2.
+
+    Returns (idx, d2, count) with idx padded by -1.
+    """
+    k = min(max_nn, len(points))
+    d, idx = tree.query(queries, k=k, distance_upper_bound=radius * (1.0 + 1e-9) + 1e-12,
+                        workers=-1)
+    if k == 1:
+        d, idx = d[:, None], idx[:, None]
+    valid = idx < len(points)
+    idx = np.where(valid, idx, 0)
+    d2 = sq_dist(queries[:, None, :], points[idx])
+    valid &= d2 < radius * radius
+    # keep the sorted-prefix semantics of std::lower_bound on the distance list
+    order = np.argsort(np.where(valid, d2, np.inf), axis=1, kind="stable")
+    idx = np.take_along_axis(idx, order, axis=1)
+    d2 = np.take_along_axis(d2, order, axis=1)
+    valid = np.take_along_axis(valid, order, axis=1)
+    idx = np.where(valid, idx, -1)
+    return idx, d2, valid.sum(axis=1)
+
+
+def compute_covariance(points, idx, count):
+    """ComputeCovariance: 9 raw cumulants / n, cov = E[pp^T] - mu mu^T; n < 3 -> identity."""
+    n = len(idx)
+    covs = np.tile(np.eye(3), (n, 1, 1))
+    ok = count >= 3
+    if not ok.any():
+        return covs
+    sel = np.flatnonzero(ok)
+    m = idx[sel] >= 0
+    P = points[np.where(m, idx[sel], 0)] * m[..., None]
+    c = count[sel].astype(np.float64)[:, None]
+    s1 = P.sum(axis=1) / c
+    xx = (P[..., 0] * P[..., 0]).sum(1) / c[:, 0]
+    xy = (P[..., 0] * P[..., 1]).sum(1) / c[:, 0]
+    xz = (P[..., 0] * P[..., 2]).sum(1) / c[:, 0]
+    yy = (P[..., 1] * P[..., 1]).sum(1) / c[:, 0]
+    yz = (P[..., 1] * P[..., 2]).sum(1) / c[:, 0]
+    zz = (P[..., 2] * P[..., 2]).sum(1) / c[:, 0]
+    C = np.empty((len(sel), 3, 3))
+    C[:, 0, 0] = xx - s1[:, 0] * s1[:, 0]
+    C[:, 1, 1] = yy - s1[:, 1] * s1[:, 1]
+    C[:, 2, 2] = zz - s1[:, 2] * s1[:, 2]
+    C[:, 0, 1] = C[:, 1, 0] = xy - s1[:, 0] * s1[:, 1]
+    C[:, 0, 2] = C[:, 2, 0] = xz - s1[:, 0] * s1[:, 2]
+    C[:, 1, 2] = C[:, 2, 1] = yz - s1[:, 1] * s1[:, 2]
+    covs[sel] = C
+    return covs
+
+
+def _cross(a, b):
+    return np.stack([a[..., 1] * b[..., 2] - a[..., 2] * b[..., 1],
+                     a[..., 2] * b[..., 0] - a[..., 0] * b[..., 2],
+                     a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]], axis=-1)
+
+
+def _dot(a, b):
+    return (a[..., 0] * b[..., 0] + a[..., 1] * b[..., 1]) + a[..., 2] * b[..., 2]
+
+
+def _eigvec0(A, e):
+    """ComputeEigenvector0: largest cross product of two shifted rows, normalised."""
+    r0 = np.stack([A[:, 0, 0] - e, A[:, 0, 1], A[:, 0, 2]], axis=-1)
+    r1 = np.stack([A[:, 0, 1], A[:, 1, 1] - e, A[:, 1, 2]], axis=-1)
+    r2 = np.stack([A[:, 0, 2], A[:, 1, 2], A[:, 2, 2] - e], axis=-1)
+    c01, c02, c12 = _cross(r0, r1), _cross(r0, r2), _cross(r1, r2)
+    d0, d1, d2 = _dot(c01, c01), _dot(c02, c02), _dot(c12, c12)
+    pick1 = d1 > d0
+    best = np.where(pick1, d1, d0)
+    pick2 = d2 > best
+    out = np.where(pick2[:, None], c12 / np.sqrt(d2)[:, None],
+                   np.where(pick1[:, None], c02 / np.sqrt(d1)[:, None], c01 / np.sqrt(d0)[:, None]))
+    return out
+
+
+def _eigvec1(A, ev0, e):
+    """ComputeEigenvector1: 2x2 reduction on the plane orthogonal to ev0."""
+    big_x = np.abs(ev0[:, 0]) > np.abs(ev0[:, 1])
+    ilx = 1.0 / np.sqrt(ev0[:, 0] * ev0[:, 0] + ev0[:, 2] * ev0[:, 2])
+    ily = 1.0 / np.sqrt(ev0[:, 1] * ev0[:, 1] + ev0[:, 2] * ev0[:, 2])
+    zero = np.zeros_like(ilx)
+    Ux = np.stack([-ev0[:, 2] * ilx, zero, ev0[:, 0] * ilx], axis=-1)
+    Uy = np.stack([zero, ev0[:, 2] * ily, -ev0[:, 1] * ily], axis=-1)
+    U = np.where(big_x[:, None], Ux, Uy)
+    V = _cross(ev0, U)
+
+    def mul(M, v):
+        return np.stack([(M[:, 0, 0] * v[:, 0] + M[:, 0, 1] * v[:, 1]) + M[:, 0, 2] * v[:, 2],
+                         (M[:, 0, 1] * v[:, 0] + M[:, 1, 1] * v[:, 1]) + M[:, 1, 2] * v[:, 2],
+                         (M[:, 0, 2] * v[:, 0] + M[:, 1, 2] * v[:, 1]) + M[:, 2, 2] * v[:, 2]],
+                        axis=-1)
+    AU, AV = mul(A, U), mul(A, V)
+    m00 = _dot(U, AU) - e
+    m01 = _dot(U, AV)
+    m11 = _dot(V, AV) - e
+    a00, a01, a11 = np.abs(m00), np.abs(m01), np.abs(m11)
+    # branch A: |m00| >= |m11|
+    r_a1_01 = m01 / m00
+    r_a1_00 = 1.0 / np.sqrt(1.0 + r_a1_01 * r_a1_01)
+    r_a1_01 = r_a1_01 * r_a1_00
+    r_a2_00 = m00 / m01
+    r_a2_01 = 1.0 / np.sqrt(1.0 + r_a2_00 * r_a2_00)
+    r_a2_00 = r_a2_00 * r_a2_01
+    use1 = a00 >= a01
+    ma01 = np.where(use1, r_a1_01, r_a2_01)
+    ma00 = np.where(use1, r_a1_00, r_a2_00)
+    outA = np.where((np.maximum(a00, a01) > 0)[:, None], ma01[:, None] * U - ma00[:, None] * V, U)
+    # branch B: |m11| > |m00|
+    r_b1_01 = m01 / m11
+    r_b1_11 = 1.0 / np.sqrt(1.0 + r_b1_01 * r_b1_01)
+    r_b1_01 = r_b1_01 * r_b1_11
+    r_b2_11 = m11 / m01
+    r_b2_01 = 1.0 / np.sqrt(1.0 + r_b2_11 * r_b2_11)
+    r_b2_11 = r_b2_11 * r_b2_01
+    useb1 = a11 >= a01
+    mb11 = np.where(useb1, r_b1_11, r_b2_11)
+    mb01 = np.where(useb1, r_b1_01, r_b2_01)
+    outB = np.where((np.maximum(a11, a01) > 0)[:, None], mb11[:, None] * U - mb01[:, None] * V, U)
+    return np.where((a00 >= a11)[:, None], outA, outB)
+
+
+def fast_eigen3x3(covs):
+    """Open3D FastEigen3x3 (Geometric Tools robust symmetric 3x3) on a batch of covariances.
+
+    Returns the eigenvector of the smallest eigenvalue (unnormalised sign, as Open3D), or the
+    zero vector where the largest coefficient is 0.
+    """
+    C = np.asarray(covs, dtype=np.float64)
+    single = C.ndim == 2
+    C = C.reshape(-1, 3, 3)
+    out = np.zeros((len(C), 3))
+    mc = C.reshape(-1, 9).max(axis=1)
+    live = mc != 0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        A = C / np.where(live, mc, 1.0)[:, None, None]
+        norm = (A[:, 0, 1] * A[:, 0, 1] + A[:, 0, 2] * A[:, 0, 2]) + A[:, 1, 2] * A[:, 1, 2]
+        q = ((A[:, 0, 0] + A[:, 1, 1]) + A[:, 2, 2]) / 3
+        b00, b11, b22 = A[:, 0, 0] - q, A[:, 1, 1] - q, A[:, 2, 2] - q
+        p = np.sqrt(((((b00 * b00 + b11 * b11) + b22 * b22) + norm * 2)) / 6)
+        c00 = b11 * b22 - A[:, 1, 2] * A[:, 1, 2]
+        c01 = A[:, 0, 1] * b22 - A[:, 1, 2] * A[:, 0, 2]
+        c02 = A[:, 0, 1] * A[:, 1, 2] - b11 * A[:, 0, 2]
+        det = ((b00 * c00 - A[:, 0, 1] * c01) + A[:, 0, 2] * c02) / (p * p * p)
+        half = np.minimum(np.maximum(det * 0.5, -1.0), 1.0)
+        ang = np.arccos(half) / 3.0
+        beta2 = np.cos(ang) * 2
+        beta0 = np.cos(ang + 2.09439510239319549) * 2
+        beta1 = -(beta0 + beta2)
+        e0, e1, e2 = q + p * beta0, q + p * beta1, q + p * beta2
+        pos = half >= 0
+        # half >= 0: start from e2
+        v2 = _eigvec0(A, e2)
+        v1p = _eigvec1(A, v2, e1)
+        res_p = np.where(((e2 < e0) & (e2 < e1))[:, None], v2,
+                         np.where(((e1 < e0) & (e1 < e2))[:, None], v1p, _cross(v1p, v2)))
+        # half < 0: start from e0
+        v0 = _eigvec0(A, e0)
+        v1n = _eigvec1(A, v0, e1)
+        res_n = np.where(((e0 < e1) & (e0 < e2))[:, None], v0,
+                         np.where(((e1 < e0) & (e1 < e2))[:, None], v1n, _cross(v0, v1n)))
+        general = np.where(pos[:, None], res_p, res_n)
+        d0, d1, d2 = A[:, 0, 0], A[:, 1, 1], A[:, 2, 2]
+        diag = np.where(((d0 < d1) & (d0 < d2))[:, None], np.array([1.0, 0.0, 0.0]),
+                        np.where(((d1 < d0) & (d1 < d2))[:, None], np.array([0.0, 1.0, 0.0]),
+                                 np.array([0.0, 0.0, 1.0])))
+        out = np.where(live[:, None], np.where((norm > 0)[:, None], general, diag), 0.0)
+    return out[0] if single else out
+
+
+def estimate_normals(points, radius=NORMAL_RADIUS, max_nn=MAX_NN, chunk=4096,
+                     return_counts=False):
+    """EstimateNormals with no prior normals: cov per point, FastEigen3x3, zero -> (0,0,1)."""
+    p = np.asarray(points, dtype=np.float64)
+    tree = cKDTree(p)
+    normals = np.empty_like(p)
+    counts = np.empty(len(p), dtype=np.int64)
+    for a in range(0, len(p), chunk):
+        q = p[a:a + chunk]
+        idx, _, cnt = hybrid_search(tree, p, q, radius, max_nn)
+        covs = compute_covariance(p, idx, cnt)
+        counts[a:a + chunk] = cnt
+        n = fast_eigen3x3(covs)
+        zero = np.sqrt(_dot(n, n)) == 0.0
+        n[zero] = (0.0, 0.0, 1.0)
+        normals[a:a + chunk] = n
+    return (normals, counts) if return_counts else normals
+
+
+# --------------------------------------------------------------------------------------------
+# a6: registration_icp (keyframe.py:246-252)  [O3D RegistrationICP]
+# --------------------------------------------------------------------------------------------
+def transform_points(T, p):
+    return p @ T[:3, :3].T + T[:3, 3]
+
+
+def correspond(tree, target, src_t, max_corr):
+    """GetRegistrationResultAndCorrespondences: 1-NN with d^2 < max_corr^2."""
+    d, idx = tree.query(src_t, k=1, distance_upper_bound=max_corr * (1.0 + 1e-9), workers=-1)
+    ok = idx < len(target)
+    si = np.flatnonzero(ok)
+    ti = idx[ok]
+    d2 = sq_dist(src_t[si], target[ti])
+    keep = d2 < max_corr * max_corr
+    si, ti, d2 = si[keep], ti[keep], d2[keep]
+    if len(si) == 0:
+        return si, ti, 0.0, 0.0
+    fitness = len(si) / len(src_t)
+    rmse = math.sqrt(d2.sum() / len(si))
+    return si, ti, fitness, rmse
+
+
+def ldlt_solve(A, b):
+    """Eigen LDLT (diagonal pivoting, unit-lower L) + pseudo-inverse of D, as Eigen's solve."""
+    A = np.array(A, dtype=np.float64)
+    n = len(A)
+    tr = list(range(n))
+    for k in range(n):
+        j = k + int(np.argmax(np.abs(np.diag(A)[k:])))
+        tr[k] = j
+        if j != k:
+            A[[k, j], :] = A[[j, k], :]
+            A[:, [k, j]] = A[:, [j, k]]
+        if k > 0:
+            t = A[k, :k] * np.diag(A)[:k]
+            A[k, k] -= A[k, :k] @ t
+            if k + 1 < n:
+                A[k + 1:, k] -= A[k + 1:, :k] @ t
+        akk = A[k, k]
+        if k == 0 and akk == 0:
+            return np.zeros(n)
+        if k + 1 < n and akk != 0:
+            A[k + 1:, k] /= akk
+    L = np.tril(A, -1) + np.eye(n)
+    D = np.diag(A).copy()
+    x = np.array(b, dtype=np.float64)
+    for k in range(n):
+        x[[k, tr[k]]] = x[[tr[k], k]]
+    for i in range(n):
+        x[i] -= L[i, :i] @ x[:i]
+    tiny = np.finfo(np.float64).tiny
+    x = np.where(np.abs(D) > tiny, x / np.where(D == 0, 1, D), 0.0)
+    for i in reversed(range(n)):
+        x[i] -= L[i + 1:, i] @ x[i + 1:]
+    for k in reversed(range(n)):
+        x[[k, tr[k]]] = x[[tr[k], k]]
+    return x
+
+
+def vec6_to_mat4(x):
+    """TransformVector6dToMatrix4d: R = Rz(x2) Ry(x1) Rx(x0), t = x3..5."""
+    a, b, g = x[0], x[1], x[2]
+    Rx = np.array([[1, 0, 0], [0, math.cos(a), -math.sin(a)], [0, math.sin(a), math.cos(a)]])
+    Ry = np.array([[math.cos(b), 0, math.sin(b)], [0, 1, 0], [-math.sin(b), 0, math.cos(b)]])
+    Rz = np.array([[math.cos(g), -math.sin(g), 0], [math.sin(g), math.cos(g), 0], [0, 0, 1]])
+    T = np.eye(4)
+    T[:3, :3] = Rz @ Ry @ Rx
+    T[:3, 3] = x[3:6]
+    return T
+
+
+def p2plane_system(src_t, target, tnormals, si, ti):
+    """TransformationEstimationPointToPlane: J = [p x n; n], r = (p - q) . n, w = 1."""
+    ps, pt, nt = src_t[si], target[ti], tnormals[ti]
+    r = np.einsum("ij,ij->i", ps - pt, nt)
+    J = np.concatenate([np.cross(ps, nt), nt], axis=1)
+    return J.T @ J, J.T @ r, r @ r
+
+
+def estimate_p2plane(src_t, target, tnormals, si, ti):
+    if len(si) == 0:
+        return np.eye(4)
+    JTJ, JTr, _ = p2plane_system(src_t, target, tnormals, si, ti)
+    return vec6_to_mat4(ldlt_solve(JTJ, -JTr))
+
+
+def umeyama(src, dst):
+    """Eigen::umeyama(src, dst, with_scaling=false) on 3 x n column sets (Kabsch + reflection fix)."""
+    n = len(src)
+    ms, md = src.mean(axis=0), dst.mean(axis=0)
+    sigma = (dst - md).T @ (src - ms) / n
+    U, _, Vt = np.linalg.svd(sigma)
+    S = np.ones(3)
+    if np.linalg.det(U) * np.linalg.det(Vt) < 0:
+        S[2] = -1
+    T = np.eye(4)
+    T[:3, :3] = U @ np.diag(S) @ Vt
+    T[:3, 3] = md - T[:3, :3] @ ms
+    return T
+
+
+def estimate_p2p(src_t, target, si, ti):
+    if len(si) == 0:
+        return np.eye(4)
+    return umeyama(src_t[si], target[ti])
+
+
+def registration_icp(source, target, max_corr=DISTANCE_THRESHOLD, init=None, method="p2plane",
+                     target_normals=None, max_iteration=30, relative_fitness=1e-6,
+                     relative_rmse=1e-6):
+    """RegistrationICP: correspond, then <= max_iteration (update, correspond, converge?) rounds.
+
+    Returns dict(transformation, fitness, inlier_rmse, n_corr, iterations, correspondences).
+    """
+    if max_corr <= 0.0:
+        raise RuntimeError("Invalid max_correspondence_distance.")
+    if method == "p2plane" and target_normals is None:
+        raise RuntimeError("TransformationEstimationPointToPlane requires pre-computed normal "
+                           "vectors for target PointCloud.")
+    src = np.asarray(source, dtype=np.float64)
+    tgt = np.asarray(target, dtype=np.float64)
+    T = np.eye(4) if init is None else np.array(init, dtype=np.float64)
+    tree = cKDTree(tgt)
+    pcd = transform_points(T, src)
+    si, ti, fit, rmse = correspond(tree, tgt, pcd, max_corr)
+    it = 0
+    for it in range(1, max_iteration + 1):
+        if method == "p2plane":
+            upd = estimate_p2plane(pcd, tgt, target_normals, si, ti)
+        else:
+            upd = estimate_p2p(pcd, tgt, si, ti)
+        T = upd @ T
+        pcd = transform_points(upd, pcd)
+        pf, pr = fit, rmse
+        si, ti, fit, rmse = correspond(tree, tgt, pcd, max_corr)
+        if abs(pf - fit) < relative_fitness and abs(pr - rmse) < relative_rmse:
+            break
+    return dict(transformation=T, fitness=fit, inlier_rmse=rmse, n_corr=len(si),
+                iterations=it, correspondences=np.stack([si, ti], axis=1))
+
+
+# --------------------------------------------------------------------------------------------
+# a10/a11: LoopClosing candidate search  (graphslam/loopclosing.py:202-268)
+# --------------------------------------------------------------------------------------------
+def _norm1(v):
+    """np.linalg.norm of a 1-D float64 3-vector: sqrt(fma(z, z, fma(y, y, x*x)))."""
+    x, y, z = (float(c) for c in v)
+    from fractions import Fraction as F
+    s = float(F(y) * F(y) + F(x * x))
+    s = float(F(z) * F(z) + F(s))
+    return math.sqrt(s)
+
+
+def find_index_backwards(positions, distance_backwards):
+    """loopclosing.py:223-237: walk back accumulating path length until > distance_backwards."""
+    d = 0.0
+    for i in reversed(range(len(positions) - 1)):
+        d += _norm1(positions[i + 1] - positions[i])
+        if d > distance_backwards:
+            return i
+    return None
+
+
+def find_candidates_within_radius(positions, index, radius_threshold):
+    """loopclosing.py:239-253: k < index with ||p_k - p_last|| < radius (row-wise norm)."""
+    if index is None:
+        return np.zeros(0, dtype=np.int64)
+    P = positions[:index] - positions[-1]
+    d = np.sqrt((P[:, 0] * P[:, 0] + P[:, 1] * P[:, 1]) + P[:, 2] * P[:, 2])
+    return np.flatnonzero(d < radius_threshold)
+
+
+def find_candidates(positions, distance_backwards, radius_threshold):
+    """loopclosing.py:213-221."""
+    idx = find_index_backwards(positions, distance_backwards)
+    return find_candidates_within_radius(positions, idx, radius_threshold), idx
+
+
+def find_feasible_triplets(positions, current_index, candidates):
+    """loopclosing.py:102-117 + look_for_valid_indexes :131-144 (1 < dindex < 80, 1 < d < 2)."""
+    out = []
+    c = np.sort(np.asarray(candidates))
+    for k in range(len(c)):
+        j1 = int(c[k])
+        for u in c[k:]:
+            u = int(u)
+            di = abs(u - j1)
+            de = _norm1(positions[j1] - positions[u])
+            if 1 < di < 80 and 1.0 < de < 2.0:
+                out.append([current_index, j1, u])
+                break
+    return out
+
+
+# --------------------------------------------------------------------------------------------
+# a9: compute_global_transformations  (artelib/homogeneousmatrix.py:184-205)
+# --------------------------------------------------------------------------------------------
+def compose_global(relative, T0=None):
+    T = np.eye(4) if T0 is None else np.array(T0, dtype=np.float64)
+    out = [T]
+    for R in relative:
+        T = T @ R
+        out.append(T)
+    return np.asarray(out)

@@ -1,0 +1,224 @@
+"""GPU parity: the HIP path (through the C ABI) against the float64 oracle on the same inputs.
+
+Bars (BASELINE.json north_star): bit-exact for the filter mask, voxel keys and loop-closure
+indices; transforms within 1e-4 (R, per element) / 1e-3 m (t); normals compared up to sign.
+"""
+import numpy as np
+import pytest
+
+from lidar_slam_arvc_amd import _lib, synthetic
+from oracle import open3d_restated as O
+
+pytestmark = pytest.mark.gpu
+
+R_TOL, T_TOL = 1e-4, 1e-3
+
+
+@pytest.fixture(scope="module")
+def seq8k():
+    return synthetic.make_sequence(3, seed=21, model=synthetic.VLP16_8K)
+
+
+@pytest.fixture(scope="module")
+def seq64k():
+    return synthetic.make_sequence(2, seed=2, model=synthetic.HDL64)
+
+
+def _prep(dev, scans, **kw):
+    ids = [dev.upload(s) for s in scans]
+    dev.preprocess(ids, _lib.prep_params(**kw))
+    return ids
+
+
+def _release(dev, ids):
+    for i in ids:
+        dev.release(i)
+
+
+# ------------------------------------------------------------------ filter (a2)
+def test_filter_bit_exact(dev, seq64k):
+    ids = _prep(dev, seq64k.scans, want_normals=False)
+    try:
+        for cid, scan in zip(ids, seq64k.scans):
+            got = dev.download(cid)
+            ref = O.filter_radius_height(scan)
+            assert got.shape == ref.shape
+            assert np.array_equal(got, ref)
+    finally:
+        _release(dev, ids)
+
+
+def test_filter_edges(dev):
+    pts = np.array([[0.5, 0.0, 0.0], [0.5000001, 0, 0], [35.0, 0, 0], [34.999998, 0, 0],
+                    [1, 1, -1.0], [1, 1, -0.9999999], [1, 1, 50.0], [1, 1, 49.999996],
+                    [np.nan, 1, 1], [1, np.inf, 1], [3, 4, 0], [0, 0, 0]], dtype=np.float32)
+    empty = np.zeros((0, 3), np.float32)
+    gone = np.array([[0.1, 0.1, 0.1]], np.float32)
+    ids = _prep(dev, [pts, empty, gone], want_normals=False)
+    try:
+        assert np.array_equal(dev.download(ids[0]), O.filter_radius_height(pts))
+        assert dev.info(ids[1])[1] == 0
+        assert dev.info(ids[2])[1] == 0
+    finally:
+        _release(dev, ids)
+
+
+# ------------------------------------------------------------------ voxel (a3)
+@pytest.mark.parametrize("v", [0.1, 0.25, 0.4])
+def test_voxel_bit_exact(dev, seq8k, v):
+    ids = _prep(dev, seq8k.scans[:2], want_normals=False, voxel_size=v)
+    try:
+        for cid, scan in zip(ids, seq8k.scans[:2]):
+            keys_ref, cent_ref = O.voxel_down_sample(O.filter_radius_height(scan), v)
+            keys = dev.voxel_keys(cid)
+            cent = dev.download(cid)
+            assert np.array_equal(keys.astype(np.int64), keys_ref)
+            assert np.array_equal(cent, cent_ref)
+    finally:
+        _release(dev, ids)
+
+
+# ------------------------------------------------------------------ normals (a4)
+def _normal_agreement(n_gpu, n_ref):
+    d = np.abs(np.sum(n_gpu * n_ref, axis=1))
+    return d
+
+
+@pytest.mark.parametrize("which", ["8k", "64k"])
+def test_normals(dev, seq8k, seq64k, which):
+    scan = (seq8k if which == "8k" else seq64k).scans[0]
+    ids = _prep(dev, [scan])
+    try:
+        xyz, nrm = dev.download(ids[0], normals=True)
+        ref_pts = O.filter_radius_height(scan)
+        assert np.array_equal(xyz, ref_pts)
+        ref_n, counts = O.estimate_normals(ref_pts, return_counts=True)
+        d = _normal_agreement(nrm, ref_n)
+        # f32 storage of the unit normal: |dot| = 1 to ~1e-7 where the spectrum is separated
+        good = d > 1.0 - 1e-5
+        assert good.mean() > 0.999, (good.mean(), np.sort(d)[:10])
+        # points whose neighbourhood was truncated to max_nn are covered
+        trunc = counts >= 300
+        if trunc.any():
+            assert good[trunc].mean() > 0.999
+    finally:
+        _release(dev, ids)
+
+
+# ------------------------------------------------------------------ ICP (a6)
+def _oracle_pair(seq, i, method, max_iteration=30):
+    tgt = O.filter_radius_height(seq.scans[i])
+    src = O.filter_radius_height(seq.scans[i + 1])
+    nrm = O.estimate_normals(tgt) if method == "p2plane" else None
+    return O.registration_icp(src, tgt, 10.0, seq.priors[i], method, nrm,
+                              max_iteration=max_iteration)
+
+
+@pytest.mark.parametrize("method", ["p2plane", "p2p"])
+@pytest.mark.parametrize("which", ["8k", "64k"])
+def test_icp_parity(dev, seq8k, seq64k, method, which):
+    seq = seq8k if which == "8k" else seq64k
+    ids = _prep(dev, seq.scans[:2], want_normals=(method == "p2plane"))
+    try:
+        got = dev.icp_batch([ids[1]], [ids[0]], seq.priors[:1], _lib.icp_params(method=method))[0]
+        ref = _oracle_pair(seq, 0, method)
+        T, R = got["transformation"], ref["transformation"]
+        assert np.abs(T[:3, :3] - R[:3, :3]).max() < R_TOL
+        assert np.abs(T[:3, 3] - R[:3, 3]).max() < T_TOL
+        assert abs(got["fitness"] - ref["fitness"]) < 1e-3
+        assert abs(got["inlier_rmse"] - ref["inlier_rmse"]) < 1e-3
+        assert abs(got["iterations"] - ref["iterations"]) <= 2
+    finally:
+        _release(dev, ids)
+
+
+def test_correspondences_single_pass(dev, seq64k):
+    """max_iteration = 0: one correspondence pass at the initial guess; compare the set."""
+    ids = _prep(dev, seq64k.scans[:2])
+    try:
+        got = dev.icp_batch([ids[1]], [ids[0]], seq64k.priors[:1],
+                            _lib.icp_params(max_iteration=0))[0]
+        corr = dev.last_correspondences()
+        ref = _oracle_pair(seq64k, 0, "p2plane", max_iteration=0)
+        rc = ref["correspondences"]
+        assert got["n_corr"] == len(rc)
+        assert abs(got["fitness"] - ref["fitness"]) < 1e-12
+        assert abs(got["inlier_rmse"] - ref["inlier_rmse"]) < 1e-6
+        a = {tuple(x) for x in corr.tolist()}
+        b = {tuple(x) for x in rc.tolist()}
+        # f32 distances may flip exact near-ties only
+        assert len(a ^ b) <= 2 * max(1, len(b) // 20000)
+    finally:
+        _release(dev, ids)
+
+
+@pytest.mark.parametrize("method", ["p2plane", "p2p"])
+def test_icp_known_transform(dev, seq8k, method):
+    tgt = O.filter_radius_height(seq8k.scans[0]).astype(np.float32)
+    D = synthetic.pose_from(0.2, -0.1, 0.03, 0.01, -0.015, 0.04)
+    src = O.transform_points(np.linalg.inv(D), tgt.astype(np.float64)).astype(np.float32)
+    ids = _prep(dev, [tgt, src], want_normals=(method == "p2plane"))
+    try:
+        got = dev.icp_batch([ids[1]], [ids[0]], None,
+                            _lib.icp_params(method=method, max_correspondence_distance=1.0,
+                                            max_iteration=60))[0]
+        assert np.abs(got["transformation"] - D).max() < 1e-5
+        assert got["fitness"] > 0.999
+    finally:
+        _release(dev, ids)
+
+
+def test_batch_equals_single_and_deterministic(dev, seq8k):
+    ids = _prep(dev, seq8k.scans)
+    try:
+        prm = _lib.icp_params()
+        batch = dev.icp_batch([ids[1], ids[2]], [ids[0], ids[1]], seq8k.priors, prm)
+        again = dev.icp_batch([ids[1], ids[2]], [ids[0], ids[1]], seq8k.priors, prm)
+        single = [dev.icp_batch([ids[k + 1]], [ids[k]], seq8k.priors[k:k + 1], prm)[0]
+                  for k in range(2)]
+        for a, b, c in zip(batch, again, single):
+            assert np.array_equal(a["transformation"], b["transformation"])
+            assert np.array_equal(a["transformation"], c["transformation"])
+            assert a["iterations"] == c["iterations"] and a["fitness"] == c["fitness"]
+    finally:
+        _release(dev, ids)
+
+
+def test_errors(dev, seq8k):
+    ids = _prep(dev, seq8k.scans[:2], want_normals=False)
+    try:
+        with pytest.raises(RuntimeError, match="normal"):
+            dev.icp_batch([ids[1]], [ids[0]], None, _lib.icp_params(method="p2plane"))
+        with pytest.raises(RuntimeError, match="max_correspondence_distance"):
+            dev.icp_batch([ids[1]], [ids[0]], None,
+                          _lib.icp_params(method="p2p", max_correspondence_distance=0.0))
+    finally:
+        _release(dev, ids)
+
+
+def test_empty_source(dev, seq8k):
+    ids = _prep(dev, [seq8k.scans[0], np.zeros((0, 3), np.float32)])
+    try:
+        got = dev.icp_batch([ids[1]], [ids[0]], seq8k.priors[:1], _lib.icp_params())[0]
+        assert got["fitness"] == 0.0 and got["inlier_rmse"] == 0.0
+        assert np.array_equal(got["transformation"], seq8k.priors[0])
+    finally:
+        _release(dev, ids)
+
+
+# ------------------------------------------------------------------ loop closure (a10/a11)
+def test_loop_candidates_bit_exact(dev):
+    rng = np.random.default_rng(5)
+    t = np.linspace(0, 4 * np.pi, 900)
+    P = np.stack([20 * np.cos(t), 20 * np.sin(t), 0.1 * rng.normal(size=len(t))], 1)
+    P[:, :2] += rng.normal(scale=0.3, size=(len(t), 2))
+    for m in [10, 300, 600, 900]:
+        idx, cand = dev.loop_candidates(P[:m], 9.0, 2.0)
+        ref_c, ref_i = O.find_candidates(P[:m], 9.0, 2.0)
+        assert idx == ref_i
+        assert np.array_equal(cand, ref_c)
+        if len(cand):
+            part = dev.loop_partners(P[:m], cand)
+            trip = O.find_feasible_triplets(P[:m], m - 1, cand)
+            got = [[m - 1, int(j1), int(j2)] for j1, j2 in zip(cand, part) if j2 >= 0]
+            assert got == trip
