@@ -1,0 +1,179 @@
+"""Benchmark: ICP keyframe-pair registrations/s on 64k-point HDL-64-style scans (BASELINE.json).
+
+One step = the reference's scan-matcher hot path (run_scanmatcher.py:196-213) over one batch of
+synthetic input already resident in HBM: pre-process P+1 keyframes (filter_radius_height +
+estimate_normals, keyframe.py:156-162), register the P consecutive pairs with point-to-plane ICP
+(keyframe.py:249-252, Open3D criteria), fetch the P relative transforms to the host and compose
+the global poses (homogeneousmatrix.py:184-205; RCCL all-gather of chunk totals when N > 1).
+Weak scaling: every GPU owns P pairs of one long sequence (distributed.py).
+
+    python bench.py [--gpus N --steps K --warmup W --pairs-per-gpu P]
+
+Prints one JSON line (rank 0) with the roofline of the NN correspondence kernel (HIP events on
+the library's own stream, SURVEY.md §8d algorithmic bytes) and a CPU baseline (the f64 oracle,
+rank 0 at N = 1 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+KERNELS = ["filter", "grid", "normals", "normals_overflow", "nn", "nn_fallback", "accumulate",
+           "solve", "voxel"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs-per-gpu", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
+    ap.add_argument("--cpu-sample-pairs", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(seq, n_pairs: int, method: str, threads: int):
+    """The f64 oracle (oracle/open3d_restated.py) on the first n_pairs pairs of the same data."""
+    from oracle import open3d_restated as O
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    O.WORKERS = threads
+    t0 = time.perf_counter()
+    pre = []
+    for k in range(n_pairs + 1):
+        pts = O.filter_radius_height(seq.scans[k])
+        nrm = O.estimate_normals(pts) if method == "p2plane" else None
+        pre.append((pts, nrm))
+    for k in range(n_pairs):
+        O.registration_icp(pre[k + 1][0], pre[k][0], 10.0, seq.priors[k], method, pre[k][1])
+    dt = time.perf_counter() - t0
+    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n_pairs} consecutive pairs (+{n_pairs + 1} keyframe pre-processes) of "
+                      f"the same synthetic HDL-64 sequence, f64 NumPy/SciPy cKDTree oracle, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group = dist.group.WORLD
+
+    from lidar_slam_arvc_amd import _lib, synthetic
+    from lidar_slam_arvc_amd.distributed import compose_global_sharded
+
+    P = args.pairs_per_gpu
+    first = rank * P
+    seq = synthetic.make_sequence(P + 1, seed=args.seed, model=synthetic.HDL64, first_index=first)
+    dev = _lib.device(local)
+    ids = [dev.upload(s) for s in seq.scans]        # raw scans resident in HBM
+    prep = _lib.prep_params(want_normals=(args.method == "p2plane"))
+    icp = _lib.icp_params(method=args.method)
+    cuda = torch.device("cuda", local)
+
+    def step():
+        n = dev.preprocess(ids, prep)
+        res = dev.icp_batch(ids[1:], ids[:-1], seq.priors, icp)
+        rel = np.stack([r["transformation"] for r in res])
+        compose_global_sharded(rel, group=group, device=cuda)
+        return n, res
+
+    for _ in range(args.warmup):
+        step()
+    dev.reset_stats()
+    dev.set_timing(True)
+    if group is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = step()
+    torch.cuda.synchronize()
+    if group is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    dev.set_timing(False)
+    if group is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=cuda)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    stats = {k: dev.kernel_stats(k) for k in KERNELS}
+    nn = stats["nn"]
+    n_pts, res = last
+    iters = [r["iterations"] for r in res]
+    out = None
+    if rank == 0:
+        achieved = nn["algo_bytes"] / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "nn_traffic.json")
+        if os.path.exists(tfile):
+            with open(tfile) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": "nn_kernel",
+                "algo_bytes_per_launch": nn["algo_bytes"] / max(nn["launches"], 1),
+                "avg_launch_ms": nn["ms"] / max(nn["launches"], 1),
+                "launches": nn["launches"]}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(seq, args.cpu_sample_pairs, args.method, args.cpu_threads)
+        ms_step = dt / args.steps * 1e3
+        out = {
+            "metric": "ICP keyframe-pair registrations/sec (64k-pt scans)",
+            "value": round(world * P * args.steps / dt, 3),
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32+f64",
+            "data": "synthetic (seeded ray-cast HDL-64 scans of a procedural scene)",
+            "config": {"workload": "hdl64_64k_p2plane_seq" if args.method == "p2plane"
+                       else "hdl64_64k_p2p_seq",
+                       "pairs_per_gpu": P, "global_pairs": world * P,
+                       "points_per_scan_post_filter": int(np.mean(n_pts)),
+                       "rays_per_scan": 65536, "method": args.method,
+                       "max_correspondence_distance": 10.0,
+                       "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "mean_icp_iterations": float(np.mean(iters)),
+            "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
+                                      for k, v in stats.items() if v["launches"]},
+        }
+        print(json.dumps(out), flush=True)
+    if group is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    for i in ids:
+        dev.release(i)
+
+
+if __name__ == "__main__":
+    main()

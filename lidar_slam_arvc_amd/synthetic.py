@@ -227,13 +227,15 @@ def make_sequence(n_keyframes: int, seed: int = 3, model: LidarModel = HDL64,
     """
     path = loop_path(path_length)
     scene = make_scene(seed, path)
-    scans, poses = [], []
-    for k in range(first_index, first_index + n_keyframes):
+
+    def one(k):
         rng = np.random.default_rng([seed, k])
         T = path_pose(path, start + k * spacing, rng)
-        poses.append(T)
-        scans.append(raycast(scene, T, model, rng))
-    poses = np.asarray(poses)
+        return T, raycast(scene, T, model, rng)
+
+    out = _parallel_map(one, range(first_index, first_index + n_keyframes))
+    poses = np.asarray([o[0] for o in out])
+    scans = [o[1] for o in out]
     priors = []
     for k in range(first_index, first_index + n_keyframes - 1):
         rng = np.random.default_rng([seed, k, 7])
@@ -258,8 +260,8 @@ def make_revisit_pairs(n_pairs: int, seed: int = 4, model: LidarModel = HDL64,
     """C4-style pairs: a pose on the loop and a revisit 0.5-2 m / <=10 deg away."""
     path = loop_path(path_length)
     scene = make_scene(seed, path)
-    tg, sc, gt, init = [], [], [], []
-    for k in range(first_index, first_index + n_pairs):
+
+    def one(k):
         rng = np.random.default_rng([seed, k])
         u = rng.uniform(0.0, path_length)
         Ti = path_pose(path, u, rng)
@@ -268,9 +270,23 @@ def make_revisit_pairs(n_pairs: int, seed: int = 4, model: LidarModel = HDL64,
         D = pose_from(off * math.cos(ang), off * math.sin(ang), 0.0, 0.0, 0.0,
                       np.deg2rad(rng.uniform(-10.0, 10.0)))
         Tj = Ti @ D
-        tg.append(raycast(scene, Ti, model, rng))
-        sc.append(raycast(scene, Tj, model, rng))
+        a = raycast(scene, Ti, model, rng)
+        b = raycast(scene, Tj, model, rng)
         rel = np.linalg.inv(Ti) @ Tj
-        gt.append(rel)
-        init.append(perturb(rel, rng, sigma_t, sigma_yaw_deg, yaw_only=True))
-    return PairSet(tg, sc, np.asarray(gt), np.asarray(init))
+        return a, b, rel, perturb(rel, rng, sigma_t, sigma_yaw_deg, yaw_only=True)
+
+    out = _parallel_map(one, range(first_index, first_index + n_pairs))
+    return PairSet([o[0] for o in out], [o[1] for o in out], np.asarray([o[2] for o in out]),
+                   np.asarray([o[3] for o in out]))
+
+
+def _parallel_map(fn, items):
+    """Thread pool map (NumPy releases the GIL in the ray-box kernels); order-preserving."""
+    from concurrent.futures import ThreadPoolExecutor
+    import os
+    items = list(items)
+    workers = max(1, min(8, os.cpu_count() or 1, len(items)))
+    if workers == 1:
+        return [fn(i) for i in items]
+    with ThreadPoolExecutor(workers) as ex:
+        return list(ex.map(fn, items))

@@ -21,6 +21,9 @@ MIN_HEIGHT, MAX_HEIGHT = -1.0, 50.0
 NORMAL_RADIUS, MAX_NN = 0.3, 300
 DISTANCE_THRESHOLD = 10.0
 
+# cKDTree worker threads (-1 = all cores). bench.py pins this to the cores it reports.
+WORKERS = -1
+
 
 # --------------------------------------------------------------------------------------------
 # a2: KeyFrame.filter_radius_height  (keyframe.py:74-94)
@@ -91,7 +94,7 @@ def hybrid_search(tree, points, queries, radius, max_nn):
     """
     k = min(max_nn, len(points))
     d, idx = tree.query(queries, k=k, distance_upper_bound=radius * (1.0 + 1e-9) + 1e-12,
-                        workers=-1)
+                        workers=WORKERS)
     if k == 1:
         d, idx = d[:, None], idx[:, None]
     valid = idx < len(points)
@@ -283,7 +286,7 @@ def transform_points(T, p):
 
 def correspond(tree, target, src_t, max_corr):
     """GetRegistrationResultAndCorrespondences: 1-NN with d^2 < max_corr^2."""
-    d, idx = tree.query(src_t, k=1, distance_upper_bound=max_corr * (1.0 + 1e-9), workers=-1)
+    d, idx = tree.query(src_t, k=1, distance_upper_bound=max_corr * (1.0 + 1e-9), workers=WORKERS)
     ok = idx < len(target)
     si = np.flatnonzero(ok)
     ti = idx[ok]
