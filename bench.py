@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-sample-pairs", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
     return ap.parse_args()
 
 
@@ -87,7 +88,7 @@ def main():
     seq = synthetic.make_sequence(P + 1, seed=args.seed, model=synthetic.HDL64, first_index=first)
     dev = _lib.device(local)
     ids = [dev.upload(s) for s in seq.scans]        # raw scans resident in HBM
-    prep = _lib.prep_params(want_normals=(args.method == "p2plane"))
+    prep = _lib.prep_params(want_normals=(args.method == "p2plane"), grid_cell=args.grid_cell)
     icp = _lib.icp_params(method=args.method)
     cuda = torch.device("cuda", local)
 

@@ -61,16 +61,44 @@ __device__ __forceinline__ void transform_point(const double *T, float4 p, doubl
     z = T[8] * px + T[9] * py + T[10] * pz + T[11];
 }
 
+__device__ __forceinline__ void try_point(const float4 t, uint32_t k, float qx, float qy, float qz,
+                                          float &bd2, int &bidx) {
+    const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    if (better(d2, int(k), bd2, bidx)) {
+        bd2 = d2;
+        bidx = int(k);
+    }
+}
+
+// Points of a cell are sorted by x (grid build). Small cells are scanned whole; larger ones are
+// entered at the query's x by binary search and walked outwards until dx^2 exceeds the best
+// squared distance (a point with dx^2 > best cannot be nearer; equality is still examined so
+// (d2, index) ties resolve exactly as a full scan would).
 __device__ __forceinline__ void scan_run(const float4 *__restrict__ xyz, uint32_t a, uint32_t b,
                                          float qx, float qy, float qz, float &bd2, int &bidx) {
-    for (uint32_t k = a; k < b; ++k) {
+    if (b - a <= 8) {
+        for (uint32_t k = a; k < b; ++k) try_point(xyz[k], k, qx, qy, qz, bd2, bidx);
+        return;
+    }
+    uint32_t lo = a, hi = b;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (xyz[mid].x < qx) lo = mid + 1;
+        else hi = mid;
+    }
+    for (uint32_t k = lo; k < b; ++k) {
         const float4 t = xyz[k];
-        const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
-        const float d2 = dx * dx + dy * dy + dz * dz;
-        if (better(d2, int(k), bd2, bidx)) {
-            bd2 = d2;
-            bidx = int(k);
-        }
+        const float dx = t.x - qx;
+        if (dx * dx > bd2) break;
+        try_point(t, k, qx, qy, qz, bd2, bidx);
+    }
+    for (uint32_t k = lo; k > a;) {
+        --k;
+        const float4 t = xyz[k];
+        const float dx = qx - t.x;
+        if (dx * dx > bd2) break;
+        try_point(t, k, qx, qy, qz, bd2, bidx);
     }
 }
 
@@ -98,6 +126,15 @@ nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
         double qx64, qy64, qz64;
         transform_point(P.T, S.xyz[i], qx64, qy64, qz64);
         const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
+        // warm start: the previous pass's nearest neighbour bounds this pass's search. The search
+        // stays exact -- the (d2, index) minimum over all points does not depend on the start.
+        const int prev = corr[P.src_off + i];
+        if (prev >= 0 && prev < G.n) {
+            const float4 t = G.xyz[prev];
+            const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
+            bd2 = dx * dx + dy * dy + dz * dz;
+            bidx = prev;
+        }
         const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
                     fz = (qz - G.oz) * G.inv_cell;
         const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
@@ -115,7 +152,7 @@ nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
             const uint32_t *cs = G.cell_start;
             // own cell first
             {
-                const int lin = (cz * G.ny + cy) * G.nx + cx;
+                const int lin = lsm_cell_lin(G.nbx, G.nby, cx, cy, cz);
                 scan_run(G.xyz, cs[lin], cs[lin + 1], qx, qy, qz, bd2, bidx);
             }
 #pragma unroll 1
@@ -130,7 +167,6 @@ nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
                     if (y < 0 || y >= G.ny) continue;
                     const float wyz = wz + (dy < 0 ? ly : (dy > 0 ? hy : 0.f)) * c2s;
                     if (wyz >= bd2) continue;
-                    const int row = (z * G.ny + y) * G.nx;
 #pragma unroll 1
                     for (int dx = -1; dx <= 1; ++dx) {
                         if ((dx | dy | dz) == 0) continue;
@@ -138,7 +174,8 @@ nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
                         if (x < 0 || x >= G.nx) continue;
                         const float w = wyz + (dx < 0 ? lx : (dx > 0 ? hx : 0.f)) * c2s;
                         if (w >= bd2) continue;
-                        scan_run(G.xyz, cs[row + x], cs[row + x + 1], qx, qy, qz, bd2, bidx);
+                        const int lin = lsm_cell_lin(G.nbx, G.nby, x, y, z);
+                        scan_run(G.xyz, cs[lin], cs[lin + 1], qx, qy, qz, bd2, bidx);
                     }
                 }
             }
@@ -195,6 +232,40 @@ __device__ __forceinline__ float gap2(float q, float lo, float hi) {
     return d * d;
 }
 
+// Chebyshev ring r of blocks around the origin block: t in [0, 24 r^2 + 2) -> offset.
+__device__ __forceinline__ void ring_offset(int r, int t, int &dx, int &dy, int &dz) {
+    if (r == 0) {
+        dx = dy = dz = 0;
+        return;
+    }
+    const int n1 = 2 * r + 1, n2 = 2 * r - 1;
+    if (t < 2 * n1 * n1) {                 // z = -r, z = +r faces
+        const int f = t / (n1 * n1), u = t % (n1 * n1);
+        dz = f ? r : -r;
+        dy = u / n1 - r;
+        dx = u % n1 - r;
+        return;
+    }
+    t -= 2 * n1 * n1;
+    if (t < 2 * n1 * n2) {                 // y = -r, y = +r faces without the z rims
+        const int f = t / (n1 * n2), u = t % (n1 * n2);
+        dy = f ? r : -r;
+        dz = u / n1 - r + 1;
+        dx = u % n1 - r;
+        return;
+    }
+    t -= 2 * n1 * n2;                      // x = -r, x = +r faces without y and z rims
+    const int f = t / (n2 * n2), u = t % (n2 * n2);
+    dx = f ? r : -r;
+    dz = u / n2 - r + 1;
+    dy = u % n2 - r + 1;
+}
+
+// Exact 1-NN for the queries the fast path could not resolve: one wave per query walks Chebyshev
+// rings of 4x4x4-cell blocks (each block one contiguous point range) outward from the query's
+// block. Lanes test 64 blocks at a time against the current best (lower-bound pruning); the
+// surviving blocks are scanned by the whole wave. Stops when every unscanned point is provably
+// farther than the best, or than max_corr.
 __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
             const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
@@ -211,79 +282,66 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
         const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
         float bd2 = q.best_d2;
         int bidx = q.best;
-        // previous box (cell ranges already fully examined); start with the 3x3x3 block or none
-        const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
-                    fz = (qz - G.oz) * G.inv_cell;
-        const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
-        const bool inside =
-            cx >= 0 && cx < G.nx && cy >= 0 && cy < G.ny && cz >= 0 && cz < G.nz;
-        int pxl = 1, pxh = 0, pyl = 1, pyh = 0, pzl = 1, pzh = 0;  // empty
-        if (inside) {
-            pxl = max(cx - 1, 0);
-            pxh = min(cx + 1, G.nx - 1);
-            pyl = max(cy - 1, 0);
-            pyh = min(cy + 1, G.ny - 1);
-            pzl = max(cz - 1, 0);
-            pzh = min(cz + 1, G.nz - 1);
-        }
-        float s = 4.f * G.cell;
-        for (int level = 0; level < 16; ++level) {
-            if (s > prm.maxc) s = prm.maxc;
-            const float h = s * G.inv_cell;
-            int xl = (int)floorf(fx - h - 1e-3f), xh = (int)floorf(fx + h + 1e-3f);
-            int yl = (int)floorf(fy - h - 1e-3f), yh = (int)floorf(fy + h + 1e-3f);
-            int zl = (int)floorf(fz - h - 1e-3f), zh = (int)floorf(fz + h + 1e-3f);
-            xl = max(xl, 0);
-            yl = max(yl, 0);
-            zl = max(zl, 0);
-            xh = min(xh, G.nx - 1);
-            yh = min(yh, G.ny - 1);
-            zh = min(zh, G.nz - 1);
-            for (int z = zl; z <= zh; ++z) {
-                const float wz = gap2(qz, G.oz + z * G.cell, G.oz + (z + 1) * G.cell);
-                if (wz >= bd2) continue;
-                for (int y = yl; y <= yh; ++y) {
-                    const float wyz = wz + gap2(qy, G.oy + y * G.cell, G.oy + (y + 1) * G.cell);
-                    if (wyz >= bd2) continue;
-                    const int row = (z * G.ny + y) * G.nx;
-                    const bool inner = (y >= pyl && y <= pyh && z >= pzl && z <= pzh);
-                    // up to two x-runs: [xl, pxl-1] and [pxh+1, xh] when the row crosses the
-                    // previous box, else [xl, xh]
-                    int ra0 = xl, rb0 = xh, ra1 = 1, rb1 = 0;
-                    if (inner && pxl <= pxh) {
-                        rb0 = min(xh, pxl - 1);
-                        ra1 = max(xl, pxh + 1);
-                        rb1 = xh;
+        const float B = G.cell * float(LSM_BLK);
+        const float gx1 = G.ox + G.nx * G.cell, gy1 = G.oy + G.ny * G.cell,
+                    gz1 = G.oz + G.nz * G.cell;
+        const float box2 = gap2(qx, G.ox, gx1) + gap2(qy, G.oy, gy1) + gap2(qz, G.oz, gz1);
+        if (box2 < prm.maxc2 && G.n > 0) {
+            const float invB = 1.f / B;
+            const int qbx = (int)floorf((qx - G.ox) * invB), qby = (int)floorf((qy - G.oy) * invB),
+                      qbz = (int)floorf((qz - G.oz) * invB);
+            auto outside = [](int v, int n) { return v < 0 ? -v : (v > n - 1 ? v - (n - 1) : 0); };
+            const int r0 = max(outside(qbx, G.nbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
+            const uint32_t *cs = G.cell_start;
+            for (int r = r0; r < 4096; ++r) {
+                const int nring = (r == 0) ? 1 : 24 * r * r + 2;
+                for (int base = 0; base < nring; base += LSM_WAVE) {
+                    const int t = base + lane;
+                    uint32_t a = 0, b = 0;
+                    if (t < nring) {
+                        int dx, dy, dz;
+                        ring_offset(r, t, dx, dy, dz);
+                        const int bx = qbx + dx, by = qby + dy, bz = qbz + dz;
+                        if (bx >= 0 && bx < G.nbx && by >= 0 && by < G.nby && bz >= 0 &&
+                            bz < G.nbz) {
+                            const float lb2 = gap2(qx, G.ox + bx * B, G.ox + (bx + 1) * B) +
+                                              gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
+                                              gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
+                            if (lb2 * 0.9999f < bd2) {
+                                const int bid = (bz * G.nby + by) * G.nbx + bx;
+                                a = cs[bid * LSM_BLK_CELLS];
+                                b = cs[(bid + 1) * LSM_BLK_CELLS];
+                            }
+                        }
                     }
-                    for (int r = 0; r < 2; ++r) {
-                        const int a = r ? ra1 : ra0, b = r ? rb1 : rb0;
-                        if (a > b) continue;
-                        const float wx = gap2(qx, G.ox + a * G.cell, G.ox + (b + 1) * G.cell);
-                        if (wyz + wx >= bd2) continue;
-                        const uint32_t pa = G.cell_start[row + a], pb = G.cell_start[row + b + 1];
-                        for (uint32_t k = pa + lane; k < pb; k += LSM_WAVE) {
-                            const float4 t = G.xyz[k];
-                            const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
-                            const float d2 = dx * dx + dy * dy + dz * dz;
+                    uint64_t mask = __ballot(b > a);
+                    while (mask) {
+                        const int src = __ffsll((unsigned long long)mask) - 1;
+                        mask &= mask - 1;
+                        const uint32_t ra = __shfl(a, src, LSM_WAVE), rb = __shfl(b, src, LSM_WAVE);
+                        for (uint32_t k = ra + lane; k < rb; k += LSM_WAVE) {
+                            const float4 t4 = G.xyz[k];
+                            const float ex = qx - t4.x, ey = qy - t4.y, ez = qz - t4.z;
+                            const float d2 = ex * ex + ey * ey + ez * ez;
                             if (better(d2, int(k), bd2, bidx)) {
                                 bd2 = d2;
                                 bidx = int(k);
                             }
                         }
                     }
+                    wave_argmin(bd2, bidx);
                 }
-                // keep the wave's best in sync so pruning tightens
-                wave_argmin(bd2, bidx);
+                // every unscanned point lies outside the block cube [qb - r, qb + r]
+                float bound = INFINITY;
+                if (qbx - r > 0) bound = fminf(bound, qx - (G.ox + (qbx - r) * B));
+                if (qbx + r + 1 < G.nbx) bound = fminf(bound, G.ox + (qbx + r + 1) * B - qx);
+                if (qby - r > 0) bound = fminf(bound, qy - (G.oy + (qby - r) * B));
+                if (qby + r + 1 < G.nby) bound = fminf(bound, G.oy + (qby + r + 1) * B - qy);
+                if (qbz - r > 0) bound = fminf(bound, qz - (G.oz + (qbz - r) * B));
+                if (qbz + r + 1 < G.nbz) bound = fminf(bound, G.oz + (qbz + r + 1) * B - qz);
+                if (bound == INFINITY || bd2 <= bound * bound * 0.99999f || bound >= prm.maxc)
+                    break;
             }
-            wave_argmin(bd2, bidx);
-            if (bd2 <= s * s * 0.99999f || s >= prm.maxc) break;
-            pxl = xl;
-            pxh = xh;
-            pyl = yl;
-            pyh = yh;
-            pzl = zl;
-            pzh = zh;
-            s *= 4.f;
         }
         if (lane == 0) {
             const int64_t g = P.src_off + q.i;
@@ -524,15 +582,25 @@ __device__ void umeyama_update(const double *tot, double D[16]) {
 __global__ void __launch_bounds__(LSM_WAVE)
 solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NNParams prm,
              int pass, const double *__restrict__ pair_bytes, uint32_t *__restrict__ active_next,
-             double *__restrict__ bytes_next) {
+             double *__restrict__ bytes_next, int32_t *__restrict__ flags) {
     PairState &P = st[blockIdx.x];
     if (!P.active) return;
     __shared__ double tot[32];
     const int lane = threadIdx.x;
-    if (lane < 30) {
-        double s = 0.0;
-        for (int b = 0; b < P.nblk; ++b) s += partials[size_t(P.blk0 + b) * LSM_ACC + lane];
-        tot[lane] = s;
+    // lane l sums blocks l, l+64, ... for every component; then a fixed-tree wave reduction per
+    // component (deterministic for a given block count)
+    double part[30];
+#pragma unroll
+    for (int k = 0; k < 30; ++k) part[k] = 0.0;
+    for (int b = lane; b < P.nblk; b += LSM_WAVE) {
+        const double *src = partials + size_t(P.blk0 + b) * LSM_ACC;
+#pragma unroll
+        for (int k = 0; k < 30; ++k) part[k] += src[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 30; ++k) {
+        const double v = lsm_wave_sum(part[k]);
+        if (lane == 0) tot[k] = v;
     }
     __syncthreads();
     if (lane != 0) return;
@@ -551,6 +619,7 @@ solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NN
     P.ncorr = int32_t(cnt);
     if (done) {
         P.active = 0;
+        flags[blockIdx.x] = 0;
         return;
     }
     double D[16];
@@ -648,11 +717,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     std::vector<CloudDev> cdev(uniq.size());
     for (size_t k = 0; k < uniq.size(); ++k) cdev[k] = uniq[k]->dev;
 
-    // pair states, block tasks (XCD-grouped: all blocks of a pair on one XCD's L2)
+    // pair states; block tasks are rebuilt for the active pairs of each pass (XCD-grouped: all
+    // blocks of a pair on one XCD's L2, lanes balanced by block count)
     std::vector<PairState> ps(npairs);
     std::vector<double> pbytes(npairs);
-    std::vector<std::vector<BlockTask>> lane_tasks(NXCD);
-    std::vector<int64_t> lane_load(NXCD, 0);
     int64_t src_off = 0;
     int32_t slot = 0;
     double bytes0 = 0.0;
@@ -668,33 +736,50 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         P.src = si[k];
         P.tgt = ti[k];
         P.src_off = src_off;
-        const int nblk = (nsrc + NN_THREADS - 1) / NN_THREADS;
         P.blk0 = slot;
-        P.nblk = nblk;
-        int lane = int(std::min_element(lane_load.begin(), lane_load.end()) - lane_load.begin());
-        for (int b = 0; b < nblk; ++b) lane_tasks[lane].push_back({int32_t(k), b * NN_THREADS, slot + b, 0});
-        lane_load[lane] += nblk;
-        slot += nblk;
+        P.nblk = (nsrc + NN_THREADS - 1) / NN_THREADS;
+        slot += P.nblk;
         src_off += nsrc;
         // SURVEY.md §8d algorithmic bytes of one NN pass of this pair
         pbytes[k] = double(nsrc) * 12.0 + double(tgt[k]->n) * 12.0 +
                     double(tgt[k]->nonempty_cells) * 8.0 + double(nsrc) * 8.0;
         bytes0 += pbytes[k];
-        if (nsrc == 0) {
-            P.nblk = 0;
-        }
     }
-    // interleave lanes: physical block b -> lane b % 8 (round-robin XCD dispatch)
-    size_t maxlen = 0;
-    for (auto &l : lane_tasks) maxlen = std::max(maxlen, l.size());
-    std::vector<BlockTask> tasks;
-    tasks.reserve(maxlen * NXCD);
-    for (size_t m = 0; m < maxlen; ++m)
-        for (int l = 0; l < NXCD; ++l)
-            tasks.push_back(m < lane_tasks[l].size() ? lane_tasks[l][m] : BlockTask{-1, 0, 0, 0});
-    // trim trailing padding
-    while (!tasks.empty() && tasks.back().pair < 0) tasks.pop_back();
-    const int ntasks = int(tasks.size());
+    auto build_tasks = [&](const std::vector<int32_t> &act) {
+        // fill the 8 XCD lanes in pair order, 1/8 of the blocks each: a pair stays on one or two
+        // XCDs (its target cloud stays in those L2s) and a lone straggler pair still spreads
+        // over the whole chip
+        std::vector<std::vector<BlockTask>> lanes(NXCD);
+        int64_t total = 0;
+        for (int64_t k = 0; k < npairs; ++k)
+            if (act[k]) total += ps[k].nblk;
+        const int64_t per = std::max<int64_t>((total + NXCD - 1) / NXCD, 1);
+        int l = 0;
+        int64_t filled = 0;
+        for (int64_t k = 0; k < npairs; ++k) {
+            if (!act[k]) continue;
+            const PairState &P = ps[k];
+            for (int b = 0; b < P.nblk; ++b) {
+                lanes[l].push_back({int32_t(k), b * NN_THREADS, P.blk0 + b, 0});
+                if (++filled == per && l < NXCD - 1) {
+                    ++l;
+                    filled = 0;
+                }
+            }
+        }
+        size_t maxlen = 0;
+        for (auto &l : lanes) maxlen = std::max(maxlen, l.size());
+        std::vector<BlockTask> t;
+        t.reserve(maxlen * NXCD);
+        for (size_t m = 0; m < maxlen; ++m)
+            for (int l = 0; l < NXCD; ++l)
+                t.push_back(m < lanes[l].size() ? lanes[l][m] : BlockTask{-1, 0, 0, 0});
+        while (!t.empty() && t.back().pair < 0) t.pop_back();
+        return t;
+    };
+    std::vector<int32_t> act(npairs, 1);
+    std::vector<BlockTask> tasks = build_tasks(act);
+    int ntasks = int(tasks.size());
     const int max_iter = p.max_iteration;
 
     CloudDev *d_cd;
@@ -720,6 +805,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     }
     uint32_t *d_qn = d_counters;            // [ncnt] fallback queue sizes per pass
     uint32_t *d_active = d_counters + ncnt; // [ncnt] active pairs after each pass
+    int32_t *d_flags;
+    if ((rc = upload(ctx, "i_flags", act, &d_flags))) return rc;
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_counters, 0, size_t(ncnt) * 2 * 4, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_bytes, 0, size_t(ncnt) * 8, st));
     if (src_off > 0) LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
@@ -736,6 +823,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     if (!h_active) return LSM_ENOMEM;
     double nn_bytes = bytes0;
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
+    int64_t nactive = npairs;
+    std::vector<int32_t> hflags(npairs);
     for (int pass = 0; pass <= max_iter && ntasks > 0; ++pass) {
         hipEvent_t ev;
         ctx->tic("nn", &ev);
@@ -756,15 +845,25 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         ctx->toc("accumulate", ev);
         ctx->tic("solve", &ev);
         solve_kernel<<<int(npairs), LSM_WAVE, 0, st>>>(d_ps, d_part, prm, pass, d_pbytes,
-                                                       d_active + pass, d_bytes + pass);
+                                                       d_active + pass, d_bytes + pass, d_flags);
         ctx->toc("solve", ev);
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(h_active, d_active + pass, 4, hipMemcpyDeviceToHost, st));
         double hb = 0.0;
         LSM_HIP_TRY(ctx, hipMemcpyAsync(h_active + 2, d_bytes + pass, 8, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(hflags.data(), d_flags, size_t(npairs) * 4,
+                                        hipMemcpyDeviceToHost, st));
         LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
         std::memcpy(&hb, h_active + 2, 8);
-        if (h_active[0] == 0) break;
+        int64_t now = 0;
+        for (int64_t k = 0; k < npairs; ++k) now += hflags[k] ? 1 : 0;
+        if (now == 0) break;
         nn_bytes += hb;
+        if (now != nactive) {      // compact the grid to the pairs still iterating
+            nactive = now;
+            for (int64_t k = 0; k < npairs; ++k) act[k] = hflags[k];
+            tasks = build_tasks(act);
+            ntasks = int(tasks.size());
+            if ((rc = upload(ctx, "i_tasks", tasks, &d_tasks))) return rc;
+        }
     }
     LSM_HIP_TRY(ctx, hipGetLastError());
     // results

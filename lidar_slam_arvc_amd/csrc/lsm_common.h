@@ -5,7 +5,10 @@
 //     by the linear index of a uniform grid cell (z-major, then y, then x), so the 3 cells of a
 //     grid row are ONE contiguous point range, and a workgroup of consecutive points covers a
 //     compact patch of space (coherent queries when the cloud is an ICP source);
-//   * a dense CSR cell table cell_start[nx*ny*nz + 1] (u32) over the cloud's own bounding box;
+//   * a dense CSR cell table cell_start[ncells + 1] (u32) over the cloud's own bounding box, with
+//     cells linearised BLOCKED: 4x4x4-cell blocks in z-major order, cells z-major inside a block.
+//     A block is one contiguous point range (the coarse level the far-field search walks), and
+//     a row of cells inside a block is contiguous too (the fine level);
 //   * normals float4 in the same order; perm[] maps sorted position -> reference (filter) order.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -23,9 +26,20 @@ struct CloudDev {
     const uint32_t *cell_start; // ncells + 1, offsets into xyz
     float ox, oy, oz;           // grid origin
     float cell, inv_cell;       // cell edge and its reciprocal
-    int nx, ny, nz;
+    int nx, ny, nz;             // cells per axis
+    int nbx, nby, nbz;          // 4x4x4 blocks per axis
     int n;
 };
+
+#define LSM_BLK 4          // cells per block edge
+#define LSM_BLK_SHIFT 2
+#define LSM_BLK_CELLS 64
+
+// blocked linear cell index (see layout note above)
+__host__ __device__ __forceinline__ int lsm_cell_lin(int nbx, int nby, int x, int y, int z) {
+    const int bx = x >> LSM_BLK_SHIFT, by = y >> LSM_BLK_SHIFT, bz = z >> LSM_BLK_SHIFT;
+    return (((bz * nby + by) * nbx + bx) << 6) | ((z & 3) << 4) | ((y & 3) << 2) | (x & 3);
+}
 
 // Per-pair ICP state (device). Layout kept 8-byte aligned.
 struct PairState {

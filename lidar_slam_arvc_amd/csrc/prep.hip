@@ -234,10 +234,11 @@ __global__ void point_cloud_ids(const uint32_t *cloud_off, const uint32_t *cloud
 struct GridGeo {
     float ox, oy, oz, cell, inv_cell;
     int nx, ny, nz;
+    int nbx, nby, nbz;
     uint32_t cell_off;     // offset of this cloud in the global cell space
     uint32_t pt_off;       // offset of this cloud in the batch point arrays
     uint32_t n;
-    uint32_t pad;
+    uint32_t ncells;       // nbx * nby * nbz * 64 (blocked, padded)
 };
 
 __device__ __forceinline__ int cell_coord(float v, float o, float inv, int nmax) {
@@ -245,7 +246,7 @@ __device__ __forceinline__ int cell_coord(float v, float o, float inv, int nmax)
 }
 
 __global__ void __launch_bounds__(PT_THREADS)
-grid_keys(const Seg *segs, const float4 *pts, const GridGeo *geo, uint32_t *keys,
+grid_keys(const Seg *segs, const float4 *pts, const GridGeo *geo, uint64_t *keys,
           uint32_t *vals) {
     const Seg s = segs[blockIdx.x];
     const GridGeo G = geo[s.cloud];
@@ -256,13 +257,17 @@ grid_keys(const Seg *segs, const float4 *pts, const GridGeo *geo, uint32_t *keys
     int cx = cell_coord(p.x, G.ox, G.inv_cell, G.nx);
     int cy = cell_coord(p.y, G.oy, G.inv_cell, G.ny);
     int cz = cell_coord(p.z, G.oz, G.inv_cell, G.nz);
-    keys[g] = G.cell_off + uint32_t((cz * G.ny + cy) * G.nx + cx);
+    // (cell, x) key: inside a cell points are ordered by x, which lets the correspondence search
+    // walk a cell outwards from the query's x and stop once dx^2 exceeds the best distance
+    uint32_t xb = __float_as_uint(p.x);
+    xb = (xb & 0x80000000u) ? ~xb : (xb | 0x80000000u);
+    keys[g] = (uint64_t(G.cell_off + uint32_t(lsm_cell_lin(G.nbx, G.nby, cx, cy, cz))) << 32) | xb;
     vals[g] = g;
 }
 
 __global__ void __launch_bounds__(PT_THREADS)
 grid_scatter(const Seg *segs, const GridGeo *geo, const CloudDev *cd, const uint32_t *svals,
-             const uint32_t *skeys, const float4 *pts, uint32_t *const *perm_out,
+             const uint64_t *skeys, const float4 *pts, uint32_t *const *perm_out,
              uint32_t *nonempty) {
     const Seg s = segs[blockIdx.x];
     const GridGeo G = geo[s.cloud];
@@ -274,7 +279,7 @@ grid_scatter(const Seg *segs, const GridGeo *geo, const CloudDev *cd, const uint
         float4 *xyz = const_cast<float4 *>(cd[s.cloud].xyz);
         xyz[j] = pts[v];
         perm_out[s.cloud][j] = v - G.pt_off;   // reference (filter / voxel-key) order
-        head = (j == 0) || (skeys[g] != skeys[g - 1]);
+        head = (j == 0) || ((skeys[g] >> 32) != (skeys[g - 1] >> 32));
     }
     uint64_t m = __ballot(head);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(&nonempty[s.cloud], (uint32_t)__popcll(m));
@@ -285,31 +290,29 @@ grid_scatter(const Seg *segs, const GridGeo *geo, const CloudDev *cd, const uint
 constexpr int FILL_CHUNK = 32;
 
 __global__ void __launch_bounds__(256)
-grid_fill(const GridGeo *geo, int ncloud, const uint32_t *skeys, uint32_t *const *cell_out) {
-    // blockIdx.y = cloud
+grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const *cell_out) {
     const int c = blockIdx.y;
     if (c >= ncloud) return;
     const GridGeo G = geo[c];
-    const int64_t ncells = int64_t(G.nx) * G.ny * G.nz;
+    const int64_t ncells = G.ncells;
     const int64_t nchunks = (ncells + 1 + FILL_CHUNK - 1) / FILL_CHUNK;
     uint32_t *out = cell_out[c];
-    const uint32_t *k = skeys + G.pt_off;
+    const uint64_t *k = skeys + G.pt_off;
     for (int64_t ch = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; ch < nchunks;
          ch += int64_t(gridDim.x) * blockDim.x) {
         const int64_t c0 = ch * FILL_CHUNK;
-        // lower_bound of (cell_off + c0)
         uint32_t lo = 0, hi = G.n;
         const uint32_t target = G.cell_off + uint32_t(c0);
         while (lo < hi) {
             uint32_t mid = (lo + hi) >> 1;
-            if (k[mid] < target) lo = mid + 1;
+            if (uint32_t(k[mid] >> 32) < target) lo = mid + 1;
             else hi = mid;
         }
         uint32_t j = lo;
         const int64_t c1 = c0 + FILL_CHUNK < ncells + 1 ? c0 + FILL_CHUNK : ncells + 1;
         for (int64_t cc = c0; cc < c1; ++cc) {
             const uint32_t t = G.cell_off + uint32_t(cc);
-            while (j < G.n && k[j] < t) ++j;
+            while (j < G.n && uint32_t(k[j] >> 32) < t) ++j;
             out[cc] = j;
         }
     }
@@ -321,8 +324,23 @@ grid_fill(const GridGeo *geo, int ncloud, const uint32_t *skeys, uint32_t *const
 struct NormalParams {
     double r2;        // radius^2 in f64 (Open3D compares d^2 < radius*radius)
     float r;          // radius (search box half-width)
+    float r2_lo;      // f32 d^2 below this: certainly inside (exact f64 test not needed)
+    float r2_hi;      // f32 d^2 above this: certainly outside
     int max_nn;
 };
+
+// d^2 < r^2 decided exactly as the f64 reference does: the f32 estimate (relative error
+// < 4e-7 for f32 inputs) settles every point farther than 4e-6 relative from the sphere; the
+// rest take the exact f64 path. Returns the exact f64 d^2 when inside (needed for selection).
+__device__ __forceinline__ bool in_ball(const NormalParams &np, float4 q, double qx, double qy,
+                                        double qz, float4 p, double &d2) {
+    const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+    const float f = dx * dx + dy * dy + dz * dz;
+    if (f > np.r2_hi) return false;
+    d2 = lsm_sqdist64(qx, qy, qz, p.x, p.y, p.z);
+    if (f < np.r2_lo) return true;
+    return d2 < np.r2;
+}
 
 // Covariance from centred cumulants (mathematically identical to Open3D's raw cumulants;
 // centring on the query point avoids f64 cancellation at 35 m coordinates).
@@ -382,59 +400,10 @@ __device__ __forceinline__ float slab_d2(float q, float o, float c, int k) {
     return d * d;
 }
 
-__global__ void __launch_bounds__(PT_THREADS)
-normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *overflow,
-               uint32_t *overflow_n, uint32_t overflow_cap) {
-    const Seg s = segs[blockIdx.x];
-    const CloudDev C = cd[s.cloud];
-    const int j = s.start + threadIdx.x;
-    if (j >= C.n) return;
-    const float4 qf = C.xyz[j];
-    const double qx = qf.x, qy = qf.y, qz = qf.z;
-    int xlo, xhi, ylo, yhi, zlo, zhi;
-    axis_range(qf.x, C.ox, C.inv_cell, np.r, C.nx, xlo, xhi);
-    axis_range(qf.y, C.oy, C.inv_cell, np.r, C.ny, ylo, yhi);
-    axis_range(qf.z, C.oz, C.inv_cell, np.r, C.nz, zlo, zhi);
-    const float prune = np.r * 1.0001f + 1e-6f;
-    const float prune2 = prune * prune;
-    Cum c = {};
-    for (int z = zlo; z <= zhi; ++z) {
-        const float dz2 = slab_d2(qf.z, C.oz, C.cell, z);
-        if (dz2 > prune2) continue;
-        for (int y = ylo; y <= yhi; ++y) {
-            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
-            if (dyz2 > prune2) continue;
-            const int row = (z * C.ny + y) * C.nx;
-            const uint32_t a = C.cell_start[row + xlo], b = C.cell_start[row + xhi + 1];
-            for (uint32_t k = a; k < b; ++k) {
-                const float4 p = C.xyz[k];
-                const double d2 = lsm_sqdist64(qx, qy, qz, p.x, p.y, p.z);
-                if (d2 < np.r2) cum_add(c, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
-            }
-        }
-    }
-    if (c.n > np.max_nn) {
-        uint32_t slot = atomicAdd(overflow_n, 1u);
-        if (slot < overflow_cap) {
-            overflow[slot] = uint32_t(s.cloud);
-            overflow[overflow_cap + slot] = uint32_t(j);
-        }
-        return;
-    }
-    float4 *nrm = const_cast<float4 *>(C.nrm);
-    nrm[j] = normal_from_cum(c);
-}
-
-// kNN truncation (Open3D SearchHybrid keeps the max_nn nearest): one wave (= one workgroup) per
-// overflowing point. Exact selection of the max_nn smallest (d2, sorted index) pairs: histogram
-// narrowing of a d2 interval [lo, hi) until the boundary bin fits in LDS, then ranking of that
-// bin's members. Bin boundaries are explicit values so the "below the bin" test and the bin
-// membership test agree bit for bit.
-constexpr int OV_BINS = 256;
-constexpr int OV_CAP = 512;
-
+// Visit the point ranges of the cells a radius-r ball around q can touch: rows of cells pruned by
+// their slab distance, each row split at block boundaries into contiguous runs f(a, b).
 template <typename F>
-__device__ __forceinline__ void scan_ball(const CloudDev &C, float4 qf, float r, int lane, F &&f) {
+__device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, float r, F &&f) {
     int xlo, xhi, ylo, yhi, zlo, zhi;
     axis_range(qf.x, C.ox, C.inv_cell, r, C.nx, xlo, xhi);
     axis_range(qf.y, C.oy, C.inv_cell, r, C.ny, ylo, yhi);
@@ -447,132 +416,148 @@ __device__ __forceinline__ void scan_ball(const CloudDev &C, float4 qf, float r,
         for (int y = ylo; y <= yhi; ++y) {
             const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
             if (dyz2 > prune2) continue;
-            const int row = (z * C.ny + y) * C.nx;
-            const uint32_t a = C.cell_start[row + xlo], b = C.cell_start[row + xhi + 1];
-            for (uint32_t k = a + lane; k < b; k += LSM_WAVE) f(k);
+            int x = xlo;
+            while (x <= xhi) {
+                const int xe = min(xhi, x | (LSM_BLK - 1));   // end of this block's row part
+                const int l0 = lsm_cell_lin(C.nbx, C.nby, x, y, z);
+                const int l1 = lsm_cell_lin(C.nbx, C.nby, xe, y, z);
+                const uint32_t a = C.cell_start[l0], b = C.cell_start[l1 + 1];
+                if (b > a) f(a, b);
+                x = xe + 1;
+            }
         }
     }
 }
 
-__device__ __forceinline__ double ov_bound(double lo, double hi, double width, int b) {
-    return b <= 0 ? lo : (b >= OV_BINS ? hi : lo + width * double(b));
+// Exact kNN truncation (Open3D SearchHybrid keeps the max_nn nearest of the ball, ordered by
+// (d2, traversal); here by (d2, sorted index)), one lane per point, no cross-lane traffic:
+//   scan 1: count + centred cumulants of the ball, and a 32-bin histogram of d2 over [0, r^2)
+//           kept in the lane's own LDS row. count <= max_nn (two thirds of the points): done.
+//   else:   pick the bin holding the max_nn-th neighbour; while it holds more than SEL_CAP
+//           points, rescan with a 32-bin histogram of that bin only (usually once);
+//   final:  rescan, accumulate everything below the bin, collect the bin's members (<= SEL_CAP)
+//           in the LDS row and add the `need` smallest by (d2, index).
+// Bin edges are explicit f64 values, so "below the bin" and "in the bin" agree bit for bit.
+constexpr int NB = 32;
+constexpr int HSTRIDE = NB + 1;   // LDS words per lane (padded: no bank conflicts across lanes)
+constexpr int SEL_CAP = 10;       // 3 words per (d2, index) entry -> 30 <= HSTRIDE
+
+__device__ __forceinline__ double sel_bound(double lo, double hi, double width, int b) {
+    return b <= 0 ? lo : (b >= NB ? hi : lo + width * double(b));
 }
 
-__device__ __forceinline__ int ov_bin(double d2, double lo, double hi, double width,
-                                      double scale) {
+__device__ __forceinline__ int sel_bin(double d2, double lo, double hi, double width, double scale) {
     int b = (int)((d2 - lo) * scale);
-    b = b < 0 ? 0 : (b >= OV_BINS ? OV_BINS - 1 : b);
-    while (b > 0 && d2 < ov_bound(lo, hi, width, b)) --b;
-    while (b < OV_BINS - 1 && d2 >= ov_bound(lo, hi, width, b + 1)) ++b;
+    b = b < 0 ? 0 : (b >= NB ? NB - 1 : b);
+    while (b > 0 && d2 < sel_bound(lo, hi, width, b)) --b;
+    while (b < NB - 1 && d2 >= sel_bound(lo, hi, width, b + 1)) ++b;
     return b;
 }
 
-__global__ void __launch_bounds__(LSM_WAVE)
-normals_overflow(const CloudDev *cd, NormalParams np, const uint32_t *overflow,
-                 const uint32_t *overflow_n, uint32_t overflow_cap) {
-    __shared__ uint32_t hist[OV_BINS];
-    __shared__ double cd2[OV_CAP];
-    __shared__ uint32_t cidx[OV_CAP];
-    __shared__ uint32_t ccnt;
-    const int lane = threadIdx.x;
-    const uint32_t total = min(*overflow_n, overflow_cap);
-    for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
-        const int cloud = int(overflow[item]);
-        const uint32_t j = overflow[overflow_cap + item];
-        const CloudDev C = cd[cloud];
-        const float4 qf = C.xyz[j];
-        const double qx = qf.x, qy = qf.y, qz = qf.z;
-        double lo = 0.0, hi = np.r2;
-        uint32_t need = uint32_t(np.max_nn);  // still to take from [lo, hi)
-        for (int iter = 0; iter < 8; ++iter) {
-            for (int b = lane; b < OV_BINS; b += LSM_WAVE) hist[b] = 0;
-            __syncthreads();
-            const double width = (hi - lo) / double(OV_BINS);
-            const double scale = double(OV_BINS) / (hi - lo);
-            scan_ball(C, qf, np.r, lane, [&](uint32_t k) {
-                const float4 p = C.xyz[k];
-                const double d2 = lsm_sqdist64(qx, qy, qz, p.x, p.y, p.z);
-                if (d2 < np.r2 && d2 >= lo && d2 < hi)
-                    atomicAdd(&hist[ov_bin(d2, lo, hi, width, scale)], 1u);
-            });
-            __syncthreads();
-            int bstar = OV_BINS - 1;
-            uint32_t before = 0;
-            if (lane == 0) {
-                uint32_t acc = 0;
-                for (int b = 0; b < OV_BINS; ++b) {
-                    if (acc + hist[b] >= need) {
-                        bstar = b;
-                        break;
-                    }
-                    acc += hist[b];
-                }
-                before = acc;
-            }
-            bstar = __shfl(bstar, 0, LSM_WAVE);
-            before = __shfl(before, 0, LSM_WAVE);
-            const uint32_t bin_count = hist[bstar];
-            const double nlo = ov_bound(lo, hi, width, bstar);
-            const double nhi = ov_bound(lo, hi, width, bstar + 1);
-            need -= before;
-            lo = nlo;
-            hi = nhi;
-            __syncthreads();
-            if (bin_count <= OV_CAP || !(hi > lo)) break;
-        }
-        // accumulate everything below lo; collect the [lo, hi) members
-        if (lane == 0) ccnt = 0;
-        __syncthreads();
-        Cum c = {};
-        scan_ball(C, qf, np.r, lane, [&](uint32_t k) {
+__global__ void __launch_bounds__(PT_THREADS)
+normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *stats) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    uint32_t *H = lds + threadIdx.x * HSTRIDE;
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int j = s.start + threadIdx.x;
+    if (j >= C.n) return;
+    const float4 qf = C.xyz[j];
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    // candidates in the ball's cells: when they cannot exceed max_nn, no selection is needed
+    uint32_t box = 0;
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b) { box += b - a; });
+    const bool hist = box > uint32_t(np.max_nn);
+    if (hist) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) H[b] = 0;
+    }
+    double lo = 0.0, hi = np.r2;
+    double width = (hi - lo) / double(NB), scale = double(NB) / (hi - lo);
+    Cum c = {};
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b) {
+        for (uint32_t k = a; k < b; ++k) {
             const float4 p = C.xyz[k];
-            const double d2 = lsm_sqdist64(qx, qy, qz, p.x, p.y, p.z);
-            if (!(d2 < np.r2)) return;
-            if (d2 < lo) {
+            double d2;
+            if (in_ball(np, qf, qx, qy, qz, p, d2)) {
                 cum_add(c, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
-            } else if (d2 < hi) {
-                uint32_t slot = atomicAdd(&ccnt, 1u);
-                if (slot < OV_CAP) {
-                    cd2[slot] = d2;
-                    cidx[slot] = k;
-                }
+                if (hist) H[sel_bin(d2, lo, hi, width, scale)] += 1;
+            }
+        }
+    });
+    float4 *nrm = const_cast<float4 *>(C.nrm);
+    if (c.n <= np.max_nn) {
+        nrm[j] = normal_from_cum(c);
+        return;
+    }
+    if (stats) atomicAdd(stats, 1u);
+    uint32_t need = uint32_t(np.max_nn);   // still to take from [lo, hi)
+    for (int it = 0; it < 8; ++it) {
+        uint32_t acc = 0;
+        int bstar = NB - 1;
+        for (int b = 0; b < NB; ++b) {
+            if (acc + H[b] >= need) {
+                bstar = b;
+                break;
+            }
+            acc += H[b];
+        }
+        const uint32_t bin_count = H[bstar];
+        need -= acc;
+        const double nlo = sel_bound(lo, hi, width, bstar), nhi = sel_bound(lo, hi, width, bstar + 1);
+        lo = nlo;
+        hi = nhi;
+        if (bin_count <= SEL_CAP || !(hi > lo)) break;
+        width = (hi - lo) / double(NB);
+        scale = double(NB) / (hi - lo);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) H[b] = 0;
+        ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b) {
+            for (uint32_t k = a; k < b; ++k) {
+                const float4 p = C.xyz[k];
+                double d2;
+                if (in_ball(np, qf, qx, qy, qz, p, d2) && d2 >= lo && d2 < hi)
+                    H[sel_bin(d2, lo, hi, width, scale)] += 1;
             }
         });
-        __syncthreads();
-        const uint32_t m = min(ccnt, (uint32_t)OV_CAP);
-        for (uint32_t e = lane; e < m; e += LSM_WAVE) {
-            const double de = cd2[e];
-            const uint32_t ie = cidx[e];
-            uint32_t rank = 0;
-            for (uint32_t f = 0; f < m; ++f) {
-                const double df = cd2[f];
-                rank += (df < de || (df == de && cidx[f] < ie)) ? 1u : 0u;
-            }
-            if (rank < need) {
-                const float4 p = C.xyz[ie];
-                cum_add(c, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
-            }
-        }
-        Cum t;
-        t.sx = lsm_wave_sum(c.sx);
-        t.sy = lsm_wave_sum(c.sy);
-        t.sz = lsm_wave_sum(c.sz);
-        t.sxx = lsm_wave_sum(c.sxx);
-        t.sxy = lsm_wave_sum(c.sxy);
-        t.sxz = lsm_wave_sum(c.sxz);
-        t.syy = lsm_wave_sum(c.syy);
-        t.syz = lsm_wave_sum(c.syz);
-        t.szz = lsm_wave_sum(c.szz);
-        int nn = c.n;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) nn += __shfl_xor(nn, off, LSM_WAVE);
-        t.n = nn;
-        if (lane == 0) {
-            float4 *nrm = const_cast<float4 *>(C.nrm);
-            nrm[j] = normal_from_cum(t);
-        }
-        __syncthreads();
     }
+    // final pass: everything below lo, plus the `need` smallest members of [lo, hi)
+    Cum f = {};
+    uint32_t m = 0;
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b) {
+        for (uint32_t k = a; k < b; ++k) {
+            const float4 p = C.xyz[k];
+            double d2;
+            if (!in_ball(np, qf, qx, qy, qz, p, d2)) continue;
+            if (d2 < lo) {
+                cum_add(f, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
+            } else if (d2 < hi) {
+                if (m < SEL_CAP) {
+                    const uint64_t bits = __double_as_longlong(d2);
+                    H[3 * m] = uint32_t(bits);
+                    H[3 * m + 1] = uint32_t(bits >> 32);
+                    H[3 * m + 2] = k;
+                }
+                ++m;
+            }
+        }
+    });
+    const uint32_t mm = m < SEL_CAP ? m : SEL_CAP;
+    for (uint32_t e = 0; e < mm; ++e) {
+        const uint64_t be = uint64_t(H[3 * e]) | (uint64_t(H[3 * e + 1]) << 32);
+        const uint32_t ke = H[3 * e + 2];
+        uint32_t rank = 0;
+        for (uint32_t g = 0; g < mm; ++g) {
+            const uint64_t bg = uint64_t(H[3 * g]) | (uint64_t(H[3 * g + 1]) << 32);
+            // positive doubles order like their bit patterns
+            rank += (bg < be || (bg == be && H[3 * g + 2] < ke)) ? 1u : 0u;
+        }
+        if (rank < need) {
+            const float4 p = C.xyz[ke];
+            cum_add(f, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
+        }
+    }
+    nrm[j] = normal_from_cum(f);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -906,7 +891,6 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         GridGeo &G = geo[k];
         G.pt_off = woff[k];
         G.n = wn[k];
-        G.pad = 0;
         G.ox = G.oy = G.oz = 0.f;
         G.nx = G.ny = G.nz = 1;
         float c = cell_req;
@@ -917,7 +901,8 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 const int64_t nx = int64_t(std::floor(ext[0] / c)) + 1;
                 const int64_t ny = int64_t(std::floor(ext[1] / c)) + 1;
                 const int64_t nz = int64_t(std::floor(ext[2] / c)) + 1;
-                if (nx * ny * nz <= MAX_CELLS_PER_CLOUD) {
+                const int64_t padded = ((nx + 3) / 4) * ((ny + 3) / 4) * ((nz + 3) / 4) * 64;
+                if (padded <= MAX_CELLS_PER_CLOUD) {
                     G.nx = int(nx);
                     G.ny = int(ny);
                     G.nz = int(nz);
@@ -931,8 +916,12 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         }
         G.cell = c;
         G.inv_cell = 1.f / c;
+        G.nbx = (G.nx + LSM_BLK - 1) / LSM_BLK;
+        G.nby = (G.ny + LSM_BLK - 1) / LSM_BLK;
+        G.nbz = (G.nz + LSM_BLK - 1) / LSM_BLK;
+        G.ncells = uint32_t(G.nbx) * G.nby * G.nbz * LSM_BLK_CELLS;
         G.cell_off = uint32_t(cell_total);
-        cell_total += uint64_t(G.nx) * G.ny * G.nz;
+        cell_total += uint64_t(G.ncells);
         if (cell_total >= (uint64_t(1) << 32) - 1) {
             ctx->set_error("batch too large for the 32-bit cell key space; split the batch");
             return LSM_EINVAL;
@@ -943,7 +932,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     for (int k = 0; k < K; ++k) {
         Cloud *c = clouds[k];
         if ((rc = ensure_cloud_buffers(ctx, c, wn[k], p.want_normals != 0))) return rc;
-        const int64_t ncells = int64_t(geo[k].nx) * geo[k].ny * geo[k].nz;
+        const int64_t ncells = int64_t(geo[k].ncells);
         if (c->cell_cap < ncells + 1 || !c->d_cell) {
             (void)hipFree(c->d_cell);
             c->d_cell = nullptr;
@@ -965,6 +954,9 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         D.nx = geo[k].nx;
         D.ny = geo[k].ny;
         D.nz = geo[k].nz;
+        D.nbx = geo[k].nbx;
+        D.nby = geo[k].nby;
+        D.nbz = geo[k].nbz;
         D.n = int(wn[k]);
         perm_ptrs[k] = c->d_perm;
         cell_ptrs[k] = c->d_cell;
@@ -982,8 +974,8 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     uint32_t ntot = 0;
     for (int k = 0; k < K; ++k) ntot = std::max(ntot, woff[k] + wn[k]);
     const size_t N = std::max<uint32_t>(ntot, 1);
-    uint32_t *k_in = (uint32_t *)ctx->buf("g_kin", N * 4);
-    uint32_t *k_out = (uint32_t *)ctx->buf("g_kout", N * 4);
+    uint64_t *k_in = (uint64_t *)ctx->buf("g_kin", N * 8);
+    uint64_t *k_out = (uint64_t *)ctx->buf("g_kout", N * 8);
     uint32_t *v_in = (uint32_t *)ctx->buf("g_vin", N * 4);
     uint32_t *v_out = (uint32_t *)ctx->buf("g_vout", N * 4);
     uint32_t *nonempty = (uint32_t *)ctx->buf("g_nonempty", size_t(K) * 4);
@@ -996,7 +988,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     if (!psegs.empty()) {
         grid_keys<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, wpts, d_geo, k_in, v_in);
         size_t tmpb = 0;
-        const int endbit = bits_for(cell_total);
+        const int endbit = 32 + bits_for(cell_total);
         LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(nullptr, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit,
                                   st));
         void *tmp = ctx->buf("sort_tmp", tmpb);
@@ -1007,7 +999,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     {
         int64_t maxcells = 0;
         for (int k = 0; k < K; ++k)
-            maxcells = std::max<int64_t>(maxcells, int64_t(geo[k].nx) * geo[k].ny * geo[k].nz + 1);
+            maxcells = std::max<int64_t>(maxcells, int64_t(geo[k].ncells) + 1);
         const int64_t chunks = (maxcells + FILL_CHUNK - 1) / FILL_CHUNK;
         const int gx = int(std::min<int64_t>((chunks + 255) / 256, 1024));
         grid_fill<<<dim3(gx, K), 256, 0, st>>>(d_geo, K, k_out, d_cell_ptrs);
@@ -1019,18 +1011,12 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         NormalParams np;
         np.r2 = p.normal_radius * p.normal_radius;
         np.r = float(p.normal_radius);
+        np.r2_lo = float(np.r2 * (1.0 - 4e-6));
+        np.r2_hi = float(np.r2 * (1.0 + 4e-6));
         np.max_nn = p.max_nn;
-        const uint32_t cap = std::max<uint32_t>(ntot, 1);
-        uint32_t *ov = (uint32_t *)ctx->buf("n_ov", size_t(cap) * 8);
-        uint32_t *ovn = (uint32_t *)ctx->buf("n_ovn", 16);
-        if (!ov || !ovn) return LSM_ENOMEM;
-        LSM_HIP_TRY(ctx, hipMemsetAsync(ovn, 0, 4, st));
         ctx->tic("normals", &ev);
-        normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, ov, ovn, cap);
+        normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, nullptr);
         ctx->toc("normals", ev);
-        ctx->tic("normals_overflow", &ev);
-        normals_overflow<<<8192, LSM_WAVE, 0, st>>>(d_cd, np, ov, ovn, cap);
-        ctx->toc("normals_overflow", ev);
     }
 
     std::vector<uint32_t> hne(K);

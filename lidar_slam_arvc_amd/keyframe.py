@@ -1,0 +1,241 @@
+"""KeyFrame drop-in (reference: keyframemanager/keyframe.py) on the MI355X registration path.
+
+Same constructor, attributes and method names as the reference's KeyFrame; the Open3D calls
+behind them are replaced by liblidarsm (include/lidarsm.h) through ctypes:
+
+    load_pointcloud            keyframe.py:41-45    PCD -> device raw cloud (kept resident)
+    filter_radius_height       keyframe.py:74-94    lsm_preprocess (filter only)
+    down_sample                keyframe.py:108-111  lsm_preprocess (filter + voxel)
+    pre_process                keyframe.py:113-124  lsm_preprocess (filter + voxel + normals)
+    local_registration_simple  keyframe.py:231-260  lsm_icp (P2P / P2Plane, Open3D criteria)
+
+``pointcloud`` / ``pointcloud_filtered`` expose ``.points`` (N x 3 float64) and ``.normals`` like
+the o3d.geometry.PointCloud the reference kept, downloaded lazily from the device cache.
+
+Deliberate divergences: an unknown ``option`` raises ValueError (the
+reference hits UnboundLocalError, keyframe.py:253-255); 'icp2planes' and 'fpfh' pre-processing
+(keyframe.py:164-229) raise NotImplementedError; ``transform`` returns a
+transformed host copy instead of mutating the device-resident filtered cloud.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .config import ICP_PARAMETERS
+from .pcd import read_pcd
+from .se3 import HomogeneousMatrix
+
+
+class HostPointCloud:
+    """Plain host point cloud (what o3d.geometry.PointCloud offered to the reference's callers)."""
+
+    def __init__(self, points, normals=None):
+        self.points = np.asarray(points, dtype=np.float64)
+        self.normals = None if normals is None else np.asarray(normals, dtype=np.float64)
+
+    def has_normals(self):
+        return self.normals is not None and len(self.normals) == len(self.points)
+
+    def __len__(self):
+        return len(self.points)
+
+    def __add__(self, other):
+        n = None
+        if self.has_normals() and other.has_normals():
+            n = np.vstack([self.normals, other.normals])
+        return HostPointCloud(np.vstack([self.points, other.points]), n)
+
+    def transform(self, T):
+        T = np.asarray(getattr(T, "array", T), dtype=np.float64)
+        self.points = self.points @ T[:3, :3].T + T[:3, 3]
+        if self.has_normals():
+            self.normals = self.normals @ T[:3, :3].T
+        return self
+
+
+class DevicePointCloud:
+    """A pre-processed cloud resident in HBM; host arrays are fetched on first access."""
+
+    def __init__(self, dev, handle, has_normals):
+        self._dev = dev
+        self._handle = handle
+        self._has_normals = has_normals
+        self._points = None
+        self._normals = None
+
+    def _fetch(self):
+        if self._has_normals:
+            self._points, self._normals = self._dev.download(self._handle, normals=True)
+        else:
+            self._points = self._dev.download(self._handle)
+
+    @property
+    def points(self):
+        if self._points is None:
+            self._fetch()
+        return self._points
+
+    @property
+    def normals(self):
+        if not self._has_normals:
+            return np.zeros((0, 3))
+        if self._normals is None:
+            self._fetch()
+        return self._normals
+
+    def has_normals(self):
+        return self._has_normals
+
+    def __len__(self):
+        return self._dev.info(self._handle)[1]
+
+    def to_host(self):
+        return HostPointCloud(self.points.copy(), self.normals.copy() if self._has_normals else None)
+
+
+class KeyFrame:
+    def __init__(self, directory, scan_time, voxel_size, device=None):
+        self.directory = directory
+        self.scan_time = scan_time
+        self.voxel_size = voxel_size
+        self.voxel_size_normals = 0.1
+        self.fpfh_threshold = 5
+        self.pointcloud = None
+        self.pointcloud_filtered = None
+        self.pointcloud_ground_plane = None
+        self.pointcloud_non_ground_plane = None
+        self.pointcloud_fpfh = None
+        self.voxel_size_normals_ground_plane = 0.5
+        self.voxel_size_normals = 0.3            # keyframe.py:33 overrides :16
+        self.max_radius = ICP_PARAMETERS.max_radius
+        self.min_radius = ICP_PARAMETERS.min_radius
+        self.max_height = ICP_PARAMETERS.max_height
+        self.min_height = ICP_PARAMETERS.min_height
+        self.plane_model = None
+        self.pre_processed = False
+        self.last_registration = None
+        self._dev = device if device is not None else _lib.device()
+        self._handle = None
+        self._source = None           # path or "memory" of the resident raw cloud
+        self._filter = None           # (radii, heights) of the current filtered cloud
+        self._prep_key = None         # parameters of the current processed cloud
+
+    # ------------------------------------------------------------------ raw cloud
+    def pcd_path(self):
+        return self.directory + "/robot0/lidar/data/" + str(self.scan_time) + ".pcd"
+
+    def load_pointcloud(self):
+        path = self.pcd_path()
+        if self._handle is not None and self._source == path:
+            return          # device keyframe cache: same file already resident
+        self.set_points(read_pcd(path), source=path)
+
+    def set_points(self, xyz, source="memory"):
+        """Attach an in-memory N x 3 scan (float32 = PCD precision) instead of reading a file."""
+        self._release()
+        xyz = np.asarray(xyz)
+        self._handle = self._dev.upload(xyz if xyz.dtype == np.float32 else
+                                        np.asarray(xyz, dtype=np.float64))
+        self._source = source
+        self.pointcloud = HostPointCloud(np.asarray(xyz, dtype=np.float64))
+        self.pointcloud_filtered = None
+        self._prep_key = None
+
+    def _release(self):
+        if self._handle is not None:
+            try:
+                self._dev.release(self._handle)
+            finally:
+                self._handle = None
+                self._source = None
+
+    def unload_pointcloud(self):
+        self._release()
+        self.pointcloud = None
+        self.pointcloud_filtered = None
+        self.pointcloud_ground_plane = None
+        self.pointcloud_non_ground_plane = None
+        self.pointcloud_fpfh = None
+        self._prep_key = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ pre-processing
+    def _params(self, radii, heights, voxel, normals):
+        r = radii if radii is not None else (self.min_radius, self.max_radius)
+        h = heights if heights is not None else (self.min_height, self.max_height)
+        return _lib.prep_params(min_radius=r[0], max_radius=r[1], min_height=h[0],
+                                max_height=h[1], voxel_size=voxel,
+                                normal_radius=self.voxel_size_normals,
+                                max_nn=ICP_PARAMETERS.max_nn, want_normals=normals)
+
+    def _run(self, radii, heights, voxel, normals):
+        if self._handle is None:
+            raise RuntimeError("KeyFrame has no point cloud loaded (call load_pointcloud)")
+        key = (tuple(radii) if radii is not None else None,
+               tuple(heights) if heights is not None else None, voxel, normals)
+        if key != self._prep_key:
+            self._dev.preprocess([self._handle], self._params(radii, heights, voxel, normals))
+            self._prep_key = key
+        self._filter = (radii, heights)
+        self.pointcloud_filtered = DevicePointCloud(self._dev, self._handle, normals)
+        return self.pointcloud_filtered
+
+    def filter_radius_height(self, radii=None, heights=None):
+        return self._run(radii, heights, None, False)
+
+    def down_sample(self):
+        if self.voxel_size is None:
+            return
+        radii, heights = self._filter if self._filter is not None else (None, None)
+        self._run(radii, heights, self.voxel_size, False)
+
+    def preprocess_icp_point_point(self):
+        self._run(None, None, self.voxel_size, False)
+
+    def preprocess_icp_point_plane(self):
+        self._run(None, None, self.voxel_size, True)
+
+    def pre_process(self, method=False):
+        if self.pre_processed:
+            return
+        if method == "icppointpoint":
+            self.preprocess_icp_point_point()
+        elif method == "icppointplane":
+            self.preprocess_icp_point_plane()
+        elif method in ("icp2planes", "fpfh"):
+            raise NotImplementedError(f"pre-processing method {method!r} is not on the MI355X "
+                                      "path yet (SURVEY.md §8f)")
+
+    # ------------------------------------------------------------------ registration
+    def registration_params(self, option):
+        m = {"pointpoint": "p2p", "pointplane": "p2plane"}.get(option)
+        if m is None:
+            raise ValueError("UNKNOWN OPTION. Should be pointpoint or pointplane")
+        return _lib.icp_params(max_correspondence_distance=ICP_PARAMETERS.distance_threshold,
+                               method=m)
+
+    def local_registration_simple(self, other, initial_transform, option="pointpoint"):
+        """ICP of `other` (source) onto `self` (target); returns T mapping other -> self."""
+        if initial_transform is None:
+            initial_transform = np.eye(4)
+        prm = self.registration_params(option)
+        for kf in (self, other):
+            if kf._handle is None or kf._prep_key is None:
+                raise RuntimeError("registration needs pre-processed keyframes (pre_process)")
+        init = np.asarray(initial_transform, dtype=np.float64).reshape(1, 16)
+        res = self._dev.icp_batch([other._handle], [self._handle], init, prm)[0]
+        self.last_registration = res
+        return HomogeneousMatrix(res["transformation"])
+
+    def transform(self, T):
+        if self.pointcloud_filtered is None:
+            raise RuntimeError("no filtered cloud")
+        pc = self.pointcloud_filtered
+        host = pc.to_host() if isinstance(pc, DevicePointCloud) else pc
+        return host.transform(T)

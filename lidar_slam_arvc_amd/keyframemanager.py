@@ -1,0 +1,118 @@
+"""KeyFrameManager drop-in (reference: keyframemanager/keyframemanager.py).
+
+Same constructor and methods (add_keyframes :20-24, add_keyframe :26-30, load_pointcloud(s)
+:32-38, unload_pointcloud :40-41, pre_process :49-50, compute_transformation :52-75, build_map
+:154-184), plus the batched forms the MI355X path is built for:
+
+* ``pre_process_batch(indices)`` -- one device pass over many keyframes;
+* ``compute_transformations(pairs, Tijs)`` -- many independent registrations in one ICP batch
+  (scan-matcher chain, loop-closure candidates).
+
+``compute_transformation`` dispatches on ``method`` exactly like the reference: 'icppointpoint'
+-> P2P, 'icppointplane' -> P2Plane; 'icp2planes' / 'fpfh' are not on the device path yet
+ and raise NotImplementedError; an unknown method prints and returns None, as in the
+reference (:70-72).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .keyframe import HostPointCloud, KeyFrame
+from .se3 import HomogeneousMatrix
+
+_OPTION = {"icppointpoint": "pointpoint", "icppointplane": "pointplane"}
+
+
+class KeyFrameManager:
+    def __init__(self, directory, scan_times, voxel_size, method="icppointplane", device=None):
+        self.directory = directory
+        self.scan_times = scan_times
+        self.keyframes = []
+        self.voxel_size = voxel_size
+        self.method = method
+        self.show_registration_result = False
+        self._dev = device if device is not None else _lib.device()
+
+    # ------------------------------------------------------------------ keyframes
+    def add_keyframes(self, keyframe_sampling):
+        for i in range(0, len(self.scan_times), keyframe_sampling):
+            self.add_keyframe(i)
+
+    def add_keyframe(self, index):
+        self.keyframes.append(KeyFrame(directory=self.directory, scan_time=self.scan_times[index],
+                                       voxel_size=self.voxel_size, device=self._dev))
+
+    def load_pointclouds(self):
+        for kf in self.keyframes:
+            kf.load_pointcloud()
+
+    def load_pointcloud(self, i):
+        self.keyframes[i].load_pointcloud()
+
+    def unload_pointcloud(self, i):
+        self.keyframes[i].unload_pointcloud()
+
+    def pre_process(self, index):
+        self.keyframes[index].pre_process(method=self.method)
+
+    def pre_process_batch(self, indices):
+        """pre_process for many keyframes in one device pass (identical results)."""
+        kfs = [self.keyframes[i] for i in indices]
+        if self.method not in _OPTION:
+            for kf in kfs:
+                kf.pre_process(method=self.method)
+            return
+        normals = self.method == "icppointplane"
+        todo = [kf for kf in kfs if kf._prep_key != (None, None, kf.voxel_size, normals)]
+        if todo:
+            prm = todo[0]._params(None, None, self.voxel_size, normals)
+            self._dev.preprocess([kf._handle for kf in todo], prm)
+        for kf in kfs:
+            kf._prep_key = (None, None, kf.voxel_size, normals)
+            kf._filter = (None, None)
+            from .keyframe import DevicePointCloud
+            kf.pointcloud_filtered = DevicePointCloud(self._dev, kf._handle, normals)
+
+    # ------------------------------------------------------------------ registration
+    def compute_transformation(self, i, j, Tij):
+        if self.method in _OPTION:
+            transform = self.keyframes[i].local_registration_simple(
+                self.keyframes[j], initial_transform=Tij.array, option=_OPTION[self.method])
+        elif self.method in ("icp2planes", "fpfh"):
+            raise NotImplementedError(f"registration method {self.method!r} is not on the "
+                                      "MI355X path yet (SURVEY.md §8f)")
+        else:
+            print("Unknown registration method")
+            transform = None
+        return transform
+
+    def compute_transformations(self, pairs, Tijs):
+        """Batched compute_transformation over independent (i, j) pairs."""
+        if self.method not in _OPTION:
+            return [self.compute_transformation(i, j, T) for (i, j), T in zip(pairs, Tijs)]
+        if len(pairs) == 0:
+            return []
+        prm = self.keyframes[pairs[0][0]].registration_params(_OPTION[self.method])
+        src = [self.keyframes[j]._handle for i, j in pairs]
+        tgt = [self.keyframes[i]._handle for i, j in pairs]
+        if any(h is None for h in src + tgt):
+            raise RuntimeError("registration needs loaded, pre-processed keyframes")
+        init = np.stack([np.asarray(getattr(T, "array", T), dtype=np.float64) for T in Tijs])
+        res = self._dev.icp_batch(src, tgt, init.reshape(-1, 16), prm)
+        for (i, j), r in zip(pairs, res):
+            self.keyframes[i].last_registration = r
+        return [HomogeneousMatrix(r["transformation"]) for r in res]
+
+    # ------------------------------------------------------------------ maps (§8f row 3)
+    def build_map(self, global_transforms, keyframe_sampling=10, radii=None, heights=None):
+        """Concatenate filtered (and voxelised) keyframes in the global frame; no rendering."""
+        radii = [0.5, 35.0] if radii is None else radii
+        heights = [-120.0, 120.0] if heights is None else heights
+        sampled = [global_transforms[i] for i in range(0, len(global_transforms), keyframe_sampling)]
+        out = HostPointCloud(np.zeros((0, 3)))
+        for kf, Ti in zip(self.keyframes, sampled):
+            kf.filter_radius_height(radii=radii, heights=heights)
+            kf.down_sample()
+            out = out + kf.transform(Ti.array)
+        return out
