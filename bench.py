@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-KERNELS = ["filter", "grid", "normals", "normals_overflow", "nn", "nn_fallback", "accumulate",
+KERNELS = ["filter", "grid", "normals", "nn", "nn_fallback", "accumulate",
            "solve", "voxel"]
 
 

@@ -442,6 +442,11 @@ constexpr int NB = 32;
 constexpr int HSTRIDE = NB + 1;   // LDS words per lane (padded: no bank conflicts across lanes)
 constexpr int SEL_CAP = 10;       // 3 words per (d2, index) entry -> 30 <= HSTRIDE
 
+// search radius covering every point with d2 < hi (slack for the f32 cell arithmetic)
+__device__ __forceinline__ float sel_radius(double hi, float r) {
+    return fminf(float(sqrt(hi)) * 1.0001f + 1e-5f, r);
+}
+
 __device__ __forceinline__ double sel_bound(double lo, double hi, double width, int b) {
     return b <= 0 ? lo : (b >= NB ? hi : lo + width * double(b));
 }
@@ -512,7 +517,8 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *s
         scale = double(NB) / (hi - lo);
 #pragma unroll
         for (int b = 0; b < NB; ++b) H[b] = 0;
-        ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b) {
+        // only d2 < hi matters from here on: scan the smaller ball of radius sqrt(hi)
+        ball_visit_runs(C, qf, sel_radius(hi, np.r), [&](uint32_t a, uint32_t b) {
             for (uint32_t k = a; k < b; ++k) {
                 const float4 p = C.xyz[k];
                 double d2;
@@ -524,7 +530,7 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *s
     // final pass: everything below lo, plus the `need` smallest members of [lo, hi)
     Cum f = {};
     uint32_t m = 0;
-    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b) {
+    ball_visit_runs(C, qf, sel_radius(hi, np.r), [&](uint32_t a, uint32_t b) {
         for (uint32_t k = a; k < b; ++k) {
             const float4 p = C.xyz[k];
             double d2;

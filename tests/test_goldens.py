@@ -1,0 +1,165 @@
+"""CPU: pin the oracle and the host-side drop-in types against vectors captured from the
+reference's own modules (tests/golden/make_golden.py). Bit-exact where the reference is
+integer/index work or identical NumPy arithmetic."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from lidar_slam_arvc_amd import se3
+from lidar_slam_arvc_amd.eurocio import EurocReader, sample_times
+from oracle import open3d_restated as O
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+G = np.load(os.path.join(HERE, "reference_goldens.npz"))
+J = json.load(open(os.path.join(HERE, "reference_goldens.json")))
+
+
+def _poses():
+    return [se3.HomogeneousMatrix(p.tolist(), se3.Euler(a.tolist()))
+            for p, a in zip(G["se3_pos"], G["se3_abg"])]
+
+
+def test_se3_construction_bit_exact():
+    Ts = _poses()
+    assert np.array_equal(np.stack([T.array for T in Ts]), G["se3_T"])
+
+
+def test_se3_ops_bit_exact():
+    Ts = [se3.HomogeneousMatrix(T.copy()) for T in G["se3_T"]]
+    n = len(Ts)
+    assert np.array_equal(np.stack([T.inv().array for T in Ts]), G["se3_inv"])
+    assert np.array_equal(np.stack([(Ts[i] * Ts[(i + 1) % n]).array for i in range(n)]),
+                          G["se3_mul"])
+    assert np.array_equal(np.stack([T.t2v(n=3) for T in Ts]), G["se3_t2v"])
+    assert np.array_equal(np.stack([np.asarray(T.Q().array, float) for T in Ts]), G["se3_Q"])
+    eul = [se3.HomogeneousMatrix(T.array.copy()).euler() for T in Ts]
+    assert np.array_equal(np.stack([np.stack([e[0].abg, e[1].abg]) for e in eul]),
+                          G["se3_euler"])
+
+
+def test_se3_transform_lists():
+    Ts = [se3.HomogeneousMatrix(T.copy()) for T in G["se3_T"]]
+    rel = se3.compute_relative_transformations(Ts)
+    assert np.array_equal(np.stack([T.array for T in rel]), G["se3_relative"])
+    glob = se3.compute_global_transformations(rel, T0=se3.HomogeneousMatrix(), Trobot_gps=None)
+    assert np.array_equal(np.stack([T.array for T in glob]), G["se3_global"])
+    # the oracle's serial product is the same arithmetic
+    assert np.allclose(O.compose_global([T.array for T in rel]), G["se3_global"], rtol=0,
+                       atol=1e-9)
+
+
+@pytest.mark.parametrize("si,dt", [(0, 0.5e9), (10, 1.0e9), (20, 0.3e9)])
+def test_sample_times(si, dt):
+    assert np.array_equal(sample_times(G["st_times"], start_index=si, delta_time=dt),
+                          G[f"st_out_{si}_{int(dt)}"])
+
+
+def test_oracle_loop_candidates_bit_exact():
+    poses = G["lc_poses"]
+    for case in J["loop_cases"]:
+        cur = case["current"]
+        P = poses[:cur + 1, :3, 3]
+        cand, idx = O.find_candidates(P, 9.0, 2.0)
+        assert idx == case["index_backwards"]
+        assert cand.tolist() == case["candidates"]
+        assert O.find_feasible_triplets(P, cur, cand) == case["triplets"]
+
+
+def test_csv_schema(tmp_path):
+    Ts = [se3.HomogeneousMatrix(T.copy()) for T in G["se3_T"][:5]]
+    er = EurocReader(str(tmp_path))
+    times = G["st_times"][:5]
+    er.save_transforms_as_csv(times, Ts, filename="/robot0/sm/rel.csv")
+    er.save_sensor_times_as_csv(times, filename="/robot0/sm/times.csv")
+    er.save_loop_closures_as_csv([[[1, 2], [3, 4]], None, [[5, 6]]], filename="/robot0/lc.csv")
+    assert open(tmp_path / "robot0/sm/rel.csv").read() == J["csv_transforms"]
+    assert open(tmp_path / "robot0/sm/times.csv").read() == J["csv_times"]
+    assert open(tmp_path / "robot0/lc.csv").read() == J["csv_loop_closures"]
+
+
+class _Pose:
+    def __init__(self, T):
+        self.T = T
+
+    def matrix(self):
+        return self.T
+
+
+class _Estimate:
+    def __init__(self, poses):
+        self.poses = poses
+
+    def exists(self, i):
+        return 0 <= i < len(self.poses)
+
+    def atPose3(self, i):
+        return _Pose(self.poses[i])
+
+
+class FakeGraph:
+    def __init__(self, poses, T0_gps):
+        self.current_estimate = _Estimate(poses)
+        self.T0_gps = T0_gps
+        self.edges = []
+
+    def add_edge(self, Tij, i, j, kind):
+        self.edges.append([int(i), int(j), kind, np.asarray(Tij.array).tolist()])
+
+
+class OracleCandidates:
+    """Test double for the device's candidate kernels, backed by the oracle (checker)."""
+
+    def loop_candidates(self, positions, distance_backwards, radius_threshold):
+        cand, idx = O.find_candidates(np.asarray(positions), distance_backwards, radius_threshold)
+        return idx, cand
+
+    def loop_partners(self, positions, candidates):
+        P = np.asarray(positions)
+        out = []
+        for k, j1 in enumerate(candidates):
+            tr = O.find_feasible_triplets(P, 0, [c for c in candidates[k:]])
+            out.append(tr[0][2] if tr and tr[0][1] == j1 else -1)
+        return np.array(out)
+
+
+class FakeKFM:
+    """Mirrors the golden generator's canned registrations (see make_golden.py)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def load_pointcloud(self, i):
+        pass
+
+    def pre_process(self, i):
+        pass
+
+    def compute_transformation(self, i, j, Tij):
+        self.calls.append((int(i), int(j)))
+        bump = se3.HomogeneousMatrix([0.002 * ((i + j) % 7), 0.0, 0.0],
+                                     se3.Euler([0, 0, 0.004 * ((i * j) % 5)]))
+        return Tij * bump
+
+
+def test_loop_closing_triangle_host_logic():
+    """The batched drop-in LoopClosing reproduces the reference's accepted edges."""
+    from lidar_slam_arvc_amd.loopclosing import LoopClosing
+    poses = G["lc_poses"]
+    T0 = se3.HomogeneousMatrix(G["lc_T0_gps"].copy())
+    for case in J["triangle_cases"]:
+        cur, seed = case["current"], case["seed"]
+        g = FakeGraph(list(poses[:cur + 1]), T0)
+        lc = LoopClosing(g, distance_backwards=9.0, radius_threshold=2.0,
+                         device=OracleCandidates())
+        kfm = FakeKFM()
+        np.random.seed(seed)
+        added = lc.loop_closing_triangle(cur, 20, kfm)
+        assert (added or []) == case["added"]
+        assert len(g.edges) == len(case["edges"])
+        for a, b in zip(g.edges, case["edges"]):
+            assert a[:3] == b[:3]
+            assert np.allclose(np.array(a[3]), np.array(b[3]), rtol=0, atol=1e-12)
+        # every distinct pair registered once (the reference repeats shared pairs)
+        assert sorted(set(kfm.calls)) == sorted(set(map(tuple, case["icp_calls"])))

@@ -1,0 +1,177 @@
+"""GPU: the reference-shaped API (KeyFrame / KeyFrameManager / LoopClosing / scan-matcher driver)
+end to end on the device, against the oracle and the reference goldens."""
+import json
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from lidar_slam_arvc_amd import datasets, se3, synthetic
+from lidar_slam_arvc_amd.keyframemanager import KeyFrameManager
+from lidar_slam_arvc_amd.loopclosing import LoopClosing
+from oracle import open3d_restated as O
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def euroc(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("euroc"))
+    seq = synthetic.make_sequence(4, seed=31, model=synthetic.VLP16_8K)
+    times = datasets.write_euroc(d, seq)
+    return d, seq, times
+
+
+@pytest.mark.parametrize("method", ["icppointplane", "icppointpoint"])
+def test_keyframemanager_matches_oracle(euroc, method):
+    d, seq, times = euroc
+    kfm = KeyFrameManager(d, np.array(times), voxel_size=None, method=method)
+    kfm.add_keyframe(0)
+    kfm.add_keyframe(1)
+    for i in range(2):
+        kfm.load_pointcloud(i)
+        kfm.pre_process(i)
+    Tij = se3.HomogeneousMatrix(seq.priors[0].copy())
+    T = kfm.compute_transformation(0, 1, Tij)
+    assert isinstance(T, se3.HomogeneousMatrix)
+    tgt = O.filter_radius_height(seq.scans[0])
+    src = O.filter_radius_height(seq.scans[1])
+    assert np.array_equal(kfm.keyframes[0].pointcloud_filtered.points, tgt)
+    m = "p2plane" if method == "icppointplane" else "p2p"
+    ref = O.registration_icp(src, tgt, 10.0, seq.priors[0], m,
+                             O.estimate_normals(tgt) if m == "p2plane" else None)
+    assert np.abs(T.array[:3, :3] - ref["transformation"][:3, :3]).max() < 1e-4
+    assert np.abs(T.array[:3, 3] - ref["transformation"][:3, 3]).max() < 1e-3
+    kfm.unload_pointcloud(0)
+    kfm.unload_pointcloud(1)
+
+
+def test_batch_api_equals_single(euroc):
+    d, seq, times = euroc
+    kfm = KeyFrameManager(d, np.array(times), voxel_size=None)
+    for i in range(4):
+        kfm.add_keyframe(i)
+        kfm.load_pointcloud(i)
+    kfm.pre_process_batch([0, 1, 2, 3])
+    pri = [se3.HomogeneousMatrix(p.copy()) for p in seq.priors]
+    batch = kfm.compute_transformations([(0, 1), (1, 2), (2, 3)], pri)
+    for k in range(3):
+        single = kfm.compute_transformation(k, k + 1, pri[k])
+        assert np.array_equal(single.array, batch[k].array)
+
+
+def test_keyframe_voxel_and_filters(euroc):
+    d, seq, times = euroc
+    kfm = KeyFrameManager(d, np.array(times), voxel_size=0.2)
+    kfm.add_keyframe(0)
+    kf = kfm.keyframes[0]
+    kf.load_pointcloud()
+    kf.filter_radius_height(radii=[1.0, 20.0], heights=[-0.8, 3.0])
+    ref = O.filter_radius_height(seq.scans[0], 1.0, 20.0, -0.8, 3.0)
+    assert np.array_equal(kf.pointcloud_filtered.points, ref)
+    kf.down_sample()
+    _, cent = O.voxel_down_sample(ref, 0.2)
+    assert np.array_equal(kf.pointcloud_filtered.points, cent)
+    kf.pre_process("icppointplane")
+    assert kf.pointcloud_filtered.has_normals()
+    assert np.allclose(np.linalg.norm(kf.pointcloud_filtered.normals, axis=1), 1.0, atol=1e-5)
+    with pytest.raises(NotImplementedError):
+        kf.pre_processed = False
+        kfm.method = "fpfh"
+        kf.pre_process("fpfh")
+    with pytest.raises(ValueError):
+        kf.local_registration_simple(kf, None, option="bogus")
+
+
+def test_scanmatcher_driver(euroc, tmp_path):
+    from lidar_slam_arvc_amd.scanmatcher import scanmatcher
+    d, seq, times = euroc
+    rel, glob = scanmatcher(d, batch=2, verbose=False)
+    assert len(rel) == len(times) - 1 and len(glob) == len(times)
+    for k, T in enumerate(rel):
+        tgt = O.filter_radius_height(seq.scans[k])
+        src = O.filter_radius_height(seq.scans[k + 1])
+        ref = O.registration_icp(src, tgt, 10.0, seq.priors[k], "p2plane",
+                                 O.estimate_normals(tgt))
+        # the driver reads its priors back from odom/data.csv (quaternion round trip)
+        assert np.abs(T.array[:3, :3] - ref["transformation"][:3, :3]).max() < 1e-4
+        assert np.abs(T.array[:3, 3] - ref["transformation"][:3, 3]).max() < 1e-3
+    df = pd.read_csv(d + "/robot0/scanmatcher/scanmatcher_global.csv")
+    assert list(df.columns) == ["Unnamed: 0", "#timestamp [ns]", "x", "y", "z", "qx", "qy", "qz",
+                                "qw"]
+    assert len(df) == len(times)
+
+
+def test_loop_candidates_device_vs_reference_goldens(dev):
+    G = np.load(os.path.join(HERE, "reference_goldens.npz"))
+    J = json.load(open(os.path.join(HERE, "reference_goldens.json")))
+    poses = G["lc_poses"]
+    for case in J["loop_cases"]:
+        P = poses[:case["current"] + 1, :3, 3]
+        idx, cand = dev.loop_candidates(P, 9.0, 2.0)
+        assert idx == case["index_backwards"]
+        assert cand.tolist() == case["candidates"]
+
+
+def test_loop_closing_triangle_on_device(dev):
+    from tests.test_goldens import FakeGraph, FakeKFM
+    G = np.load(os.path.join(HERE, "reference_goldens.npz"))
+    J = json.load(open(os.path.join(HERE, "reference_goldens.json")))
+    T0 = se3.HomogeneousMatrix(G["lc_T0_gps"].copy())
+    for case in J["triangle_cases"]:
+        g = FakeGraph(list(G["lc_poses"][:case["current"] + 1]), T0)
+        lc = LoopClosing(g, distance_backwards=9.0, radius_threshold=2.0, device=dev)
+        np.random.seed(case["seed"])
+        added = lc.loop_closing_triangle(case["current"], 20, FakeKFM())
+        assert (added or []) == case["added"]
+        assert [e[:3] for e in g.edges] == [e[:3] for e in case["edges"]]
+
+
+def test_loop_closing_real_icp_batch(dev):
+    """Revisit pairs (C4-style, HDL-64) through the batched KeyFrameManager path with real ICP.
+
+    These registrations converge (7-10 updates); see test_nonconverged_pairs for the others."""
+    ps = synthetic.make_revisit_pairs(3, seed=4, model=synthetic.HDL64)
+    kfm = KeyFrameManager("unused", np.arange(6), voxel_size=None, device=dev)
+    for k in range(3):
+        kfm.add_keyframe(2 * k)
+        kfm.add_keyframe(2 * k + 1)
+        kfm.keyframes[2 * k].set_points(ps.targets[k])
+        kfm.keyframes[2 * k + 1].set_points(ps.sources[k])
+    kfm.pre_process_batch(range(6))
+    res = kfm.compute_transformations([(0, 1), (2, 3), (4, 5)],
+                                      [se3.HomogeneousMatrix(T.copy()) for T in ps.init])
+    for k, T in enumerate(res):
+        tgt = O.filter_radius_height(ps.targets[k])
+        src = O.filter_radius_height(ps.sources[k])
+        ref = O.registration_icp(src, tgt, 10.0, ps.init[k], "p2plane", O.estimate_normals(tgt))
+        assert np.abs(T.array[:3, :3] - ref["transformation"][:3, :3]).max() < 1e-4
+        assert np.abs(T.array[:3, 3] - ref["transformation"][:3, 3]).max() < 1e-3
+
+
+def test_nonconverged_pairs_agree_in_quality(dev):
+    """Sparse 16-ring revisit pairs that hit max_iteration = 30 without converging are chaotic:
+    perturbing the oracle's own normals by 1e-7 moves its answer by ~1e-3,
+    so Open3D's OpenMP reduction order makes them irreproducible in the reference too. For those
+    the bar is equal quality: fitness equal to 1e-3 and an rmse no worse than 5 % above the
+    oracle's (the device may stop earlier: the convergence test itself is chaotic there)."""
+    ps = synthetic.make_revisit_pairs(3, seed=41, model=synthetic.VLP16_8K)
+    ids = []
+    try:
+        for k in range(3):
+            ids += [dev.upload(ps.targets[k]), dev.upload(ps.sources[k])]
+        from lidar_slam_arvc_amd import _lib
+        dev.preprocess(ids, _lib.prep_params())
+        res = dev.icp_batch(ids[1::2], ids[0::2], ps.init, _lib.icp_params())
+        for k, g in enumerate(res):
+            tgt = O.filter_radius_height(ps.targets[k])
+            src = O.filter_radius_height(ps.sources[k])
+            r = O.registration_icp(src, tgt, 10.0, ps.init[k], "p2plane", O.estimate_normals(tgt))
+            assert r["iterations"] == 30                 # the oracle did not converge
+            assert abs(g["fitness"] - r["fitness"]) < 1e-3
+            assert g["inlier_rmse"] < 1.05 * r["inlier_rmse"]
+    finally:
+        for i in ids:
+            dev.release(i)

@@ -1,0 +1,166 @@
+"""CPU: the C-ABI library (load + exported symbols, no compute), host logic, data formats, and
+the multi-rank pose composition over gloo."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from lidar_slam_arvc_amd import _lib, distributed, pcd, synthetic
+from oracle import open3d_restated as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "lidarsm.h")).read()
+    return sorted(set(re.findall(r"\b(lsm_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load_library()
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(_lib.EXPORTED) == syms
+
+
+def test_struct_layouts_match_header():
+    assert C.sizeof(_lib.PrepParams) == 6 * 8 + 2 * 4 + 8
+    assert C.sizeof(_lib.IcpParams) == 8 + 2 * 4 + 2 * 8
+    assert C.sizeof(_lib.IcpResult) == 16 * 8 + 2 * 8 + 8 + 2 * 4
+
+
+def test_defaults_follow_icp_parameters():
+    lib = _lib.load_library()
+    p = _lib.PrepParams()
+    lib.lsm_default_prep_params(C.byref(p))
+    assert (p.min_radius, p.max_radius, p.min_height, p.max_height) == (0.5, 35.0, -1.0, 50.0)
+    assert (p.normal_radius, p.max_nn, p.voxel_size, p.want_normals) == (0.3, 300, 0.0, 1)
+    q = _lib.IcpParams()
+    lib.lsm_default_icp_params(C.byref(q))
+    assert (q.max_correspondence_distance, q.method, q.max_iteration) == (10.0, 1, 30)
+    assert (q.relative_fitness, q.relative_rmse) == (1e-6, 1e-6)
+    assert lib.lsm_version().decode().startswith("liblidarsm")
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="no usable gfx950 device"):
+        _lib.Device(0)
+
+
+def test_params_helpers():
+    assert _lib.icp_params(method="pointpoint").method == _lib.LSM_P2P
+    assert _lib.icp_params(method="pointplane").method == _lib.LSM_P2PLANE
+    with pytest.raises(ValueError):
+        _lib.icp_params(method="fpfh")
+    assert _lib.prep_params(voxel_size=None).voxel_size == 0.0
+
+
+def test_config_matches_reference_values():
+    from lidar_slam_arvc_amd.config import ICP_PARAMETERS as P
+    assert (P.max_radius, P.min_radius, P.max_height, P.min_height) == (35, 0.5, 50.0, -1.0)
+    assert (P.voxel_size, P.max_nn, P.distance_threshold) == (None, 300, 10.0)
+
+
+# ------------------------------------------------------------------ data formats
+@pytest.mark.parametrize("mode", ["ascii", "binary"])
+def test_pcd_roundtrip(tmp_path, mode):
+    rng = np.random.default_rng(0)
+    p = (rng.normal(size=(500, 3)) * 10).astype(np.float32)
+    p[3] = [np.nan, 1, 2]
+    f = tmp_path / f"a_{mode}.pcd"
+    pcd.write_pcd(str(f), p, mode)
+    q = pcd.read_pcd(str(f))
+    assert q.dtype == np.float32 and q.shape == p.shape
+    assert np.array_equal(q, p, equal_nan=True)
+
+
+def _lzf_compress_literals(data: bytes) -> bytes:
+    out = bytearray()
+    for i in range(0, len(data), 32):
+        chunk = data[i:i + 32]
+        out.append(len(chunk) - 1)
+        out += chunk
+    return bytes(out)
+
+
+def test_pcd_binary_compressed(tmp_path):
+    rng = np.random.default_rng(1)
+    p = (rng.normal(size=(64, 3)) * 3).astype(np.float32)
+    cols = b"".join(np.ascontiguousarray(p[:, k]).tobytes() for k in range(3))
+    comp = _lzf_compress_literals(cols)
+    head = ("VERSION 0.7\nFIELDS x y z\nSIZE 4 4 4\nTYPE F F F\nCOUNT 1 1 1\nWIDTH 64\n"
+            "HEIGHT 1\nPOINTS 64\nDATA binary_compressed\n").encode()
+    f = tmp_path / "c.pcd"
+    f.write_bytes(head + np.array([len(comp), len(cols)], "<u4").tobytes() + comp)
+    assert np.array_equal(pcd.read_pcd(str(f)), p)
+
+
+def test_lzf_backreference():
+    # literal "abc" then a back-reference of length 6 at distance 3 -> "abcabcabc"
+    src = bytes([2]) + b"abc" + bytes([(4 << 5) | 0, 2])
+    assert pcd.lzf_decompress(src, 9) == b"abcabcabc"
+
+
+# ------------------------------------------------------------------ synthetic data
+def test_synthetic_determinism_and_chunking():
+    a = synthetic.make_sequence(4, seed=9, model=synthetic.VLP16_8K)
+    b = synthetic.make_sequence(2, seed=9, model=synthetic.VLP16_8K, first_index=2)
+    assert np.array_equal(a.scans[2], b.scans[0]) and np.array_equal(a.scans[3], b.scans[1])
+    assert np.array_equal(a.poses[2:], b.poses)
+    assert np.array_equal(a.priors[2], b.priors[0])
+    for s in a.scans:
+        assert s.dtype == np.float32 and s.shape[1] == 3 and len(s) > 1000
+    gt = np.linalg.inv(a.poses[0]) @ a.poses[1]
+    assert np.abs(gt[:3, 3] - a.priors[0][:3, 3]).max() < 0.5
+
+
+# ------------------------------------------------------------------ sharding
+def test_shard_pairs_cover():
+    for n in [1, 7, 64, 1999]:
+        for w in [1, 2, 3, 8]:
+            rs = [distributed.shard_pairs(n, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            for (a, b), (c, d) in zip(rs, rs[1:]):
+                assert b == c and a <= b
+
+
+def _gloo_worker(rank, world, port, rel, out_q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a, b = distributed.shard_pairs(len(rel), world, rank)
+    poses = distributed.compose_global_sharded(rel[a:b])
+    out_q.put((rank, a, poses))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_compose_global_sharded_gloo(world):
+    import multiprocessing as mp
+    import socket
+    rng = np.random.default_rng(world)
+    rel = np.stack([synthetic.pose_from(*rng.normal(size=3), *rng.normal(scale=0.1, size=3))
+                    for _ in range(23)])
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, world, port, rel, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    serial = O.compose_global(rel)
+    for rank, a, poses in got:
+        assert np.allclose(poses, serial[a:a + len(poses)], rtol=0, atol=1e-9)
