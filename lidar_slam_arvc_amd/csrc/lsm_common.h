@@ -86,6 +86,29 @@ __device__ __forceinline__ double lsm_sqdist64(double qx, double qy, double qz, 
     return __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
 }
 
+// Loads through a global-address-space view of a device pointer that was read from a
+// descriptor (CloudDev, PairState tables): the compiler then emits global_load (counted by
+// vmcnt only) instead of flat_load, whose lgkmcnt share serialises it with LDS traffic.
+// (The host pass of hipcc only type-checks device code; it has no address spaces.)
+template <typename T>
+__device__ __forceinline__ T lsm_ld(const T *p, size_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const __attribute__((address_space(1))) T *)p)[i];
+#else
+    return p[i];
+#endif
+}
+
+__device__ __forceinline__ float4 lsm_ld(const float4 *p, size_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    const v4 v = ((const __attribute__((address_space(1))) v4 *)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return p[i];
+#endif
+}
+
 __device__ __forceinline__ int lsm_clampi(int v, int lo, int hi) {
     return v < lo ? lo : (v > hi ? hi : v);
 }

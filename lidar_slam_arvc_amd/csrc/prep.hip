@@ -329,17 +329,36 @@ struct NormalParams {
     int max_nn;
 };
 
+// Offsets of a candidate from the query in f64 (exact: both are f32 values) with their squares,
+// and the exact nanoflann d^2 = ((dx^2 + dy^2) + dz^2) built from the same products
+// (lsm_sqdist64 bit for bit: (p - q)^2 == (q - p)^2).
+struct Off {
+    double dx, dy, dz, xx, yy, zz, d2;
+};
+
+__device__ __forceinline__ Off make_off(float4 p, double qx, double qy, double qz) {
+    Off o;
+    o.dx = __dsub_rn((double)p.x, qx);
+    o.dy = __dsub_rn((double)p.y, qy);
+    o.dz = __dsub_rn((double)p.z, qz);
+    o.xx = __dmul_rn(o.dx, o.dx);
+    o.yy = __dmul_rn(o.dy, o.dy);
+    o.zz = __dmul_rn(o.dz, o.dz);
+    o.d2 = __dadd_rn(__dadd_rn(o.xx, o.yy), o.zz);
+    return o;
+}
+
 // d^2 < r^2 decided exactly as the f64 reference does: the f32 estimate (relative error
 // < 4e-7 for f32 inputs) settles every point farther than 4e-6 relative from the sphere; the
-// rest take the exact f64 path. Returns the exact f64 d^2 when inside (needed for selection).
+// rest take the exact f64 value. The f64 offsets are computed once and shared with the
+// cumulants and the selection binning.
 __device__ __forceinline__ bool in_ball(const NormalParams &np, float4 q, double qx, double qy,
-                                        double qz, float4 p, double &d2) {
+                                        double qz, float4 p, Off &o) {
     const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
     const float f = dx * dx + dy * dy + dz * dz;
     if (f > np.r2_hi) return false;
-    d2 = lsm_sqdist64(qx, qy, qz, p.x, p.y, p.z);
-    if (f < np.r2_lo) return true;
-    return d2 < np.r2;
+    o = make_off(p, qx, qy, qz);
+    return f < np.r2_lo || o.d2 < np.r2;
 }
 
 // Covariance from centred cumulants (mathematically identical to Open3D's raw cumulants;
@@ -349,16 +368,16 @@ struct Cum {
     int n;
 };
 
-__device__ __forceinline__ void cum_add(Cum &c, double dx, double dy, double dz) {
-    c.sx += dx;
-    c.sy += dy;
-    c.sz += dz;
-    c.sxx += dx * dx;
-    c.sxy += dx * dy;
-    c.sxz += dx * dz;
-    c.syy += dy * dy;
-    c.syz += dy * dz;
-    c.szz += dz * dz;
+__device__ __forceinline__ void cum_add(Cum &c, const Off &o) {
+    c.sx += o.dx;
+    c.sy += o.dy;
+    c.sz += o.dz;
+    c.sxx += o.xx;
+    c.syy += o.yy;
+    c.szz += o.zz;
+    c.sxy = fma(o.dx, o.dy, c.sxy);
+    c.sxz = fma(o.dx, o.dz, c.sxz);
+    c.syz = fma(o.dy, o.dz, c.syz);
     c.n += 1;
 }
 
@@ -401,7 +420,10 @@ __device__ __forceinline__ float slab_d2(float q, float o, float c, int k) {
 }
 
 // Visit the point ranges of the cells a radius-r ball around q can touch: rows of cells pruned by
-// their slab distance, each row split at block boundaries into contiguous runs f(a, b).
+// their slab distance, each row split at block boundaries into contiguous runs f(a, b, xl, xh).
+// A run is sorted by x (cells of a row are x-ordered and each cell is x-sorted; the f32 cell
+// index is monotone in x), and every ball point of the row has xl <= x <= xh (the chord of the
+// row's nearest slab, widened for f32 rounding), so f may skip x < xl and stop at x > xh.
 template <typename F>
 __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, float r, F &&f) {
     int xlo, xhi, ylo, yhi, zlo, zhi;
@@ -416,137 +438,247 @@ __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, fl
         for (int y = ylo; y <= yhi; ++y) {
             const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
             if (dyz2 > prune2) continue;
+            const float ch = sqrtf(prune2 - dyz2) * 1.0001f + 1e-6f * fabsf(qf.x) + 1e-5f;
+            const float xl = qf.x - ch, xh = qf.x + ch;
             int x = xlo;
             while (x <= xhi) {
                 const int xe = min(xhi, x | (LSM_BLK - 1));   // end of this block's row part
                 const int l0 = lsm_cell_lin(C.nbx, C.nby, x, y, z);
                 const int l1 = lsm_cell_lin(C.nbx, C.nby, xe, y, z);
-                const uint32_t a = C.cell_start[l0], b = C.cell_start[l1 + 1];
-                if (b > a) f(a, b);
+                const uint32_t a = lsm_ld(C.cell_start, l0), b = lsm_ld(C.cell_start, l1 + 1);
+                if (b > a) f(a, b, xl, xh);
                 x = xe + 1;
             }
         }
     }
 }
 
+// One x-sorted run [a, b) of a row with its window [xl, xh]: body(p, k) for every point in the
+// window. Long runs find the window's first point by binary search on x (a run averages ~140
+// points of which ~30 lie left of the window on HDL-64 scans); the walk stops past xh.
+constexpr uint32_t SCAN_BSEARCH = 16;
+
+template <typename Body>
+__device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float xl, float xh,
+                                         Body &&body) {
+    if (b - a > SCAN_BSEARCH) {
+        uint32_t lo = a, hi = b;
+        const float *xs = reinterpret_cast<const float *>(xyz);
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (lsm_ld(xs, size_t(mid) * 4) < xl) lo = mid + 1;
+            else hi = mid;
+        }
+        a = lo;
+    }
+    for (uint32_t k = a; k < b; ++k) {
+        const float4 p = lsm_ld(xyz, k);
+        if (p.x > xh) break;
+        if (p.x >= xl) body(p, k);
+    }
+}
+
 // Exact kNN truncation (Open3D SearchHybrid keeps the max_nn nearest of the ball, ordered by
-// (d2, traversal); here by (d2, sorted index)), one lane per point, no cross-lane traffic:
-//   scan 1: count + centred cumulants of the ball, and a 32-bin histogram of d2 over [0, r^2)
-//           kept in the lane's own LDS row. count <= max_nn (two thirds of the points): done.
-//   else:   pick the bin holding the max_nn-th neighbour; while it holds more than SEL_CAP
-//           points, rescan with a 32-bin histogram of that bin only (usually once);
-//   final:  rescan, accumulate everything below the bin, collect the bin's members (<= SEL_CAP)
-//           in the LDS row and add the `need` smallest by (d2, index).
-// Bin edges are explicit f64 values, so "below the bin" and "in the bin" agree bit for bit.
-constexpr int NB = 32;
-constexpr int HSTRIDE = NB + 1;   // LDS words per lane (padded: no bank conflicts across lanes)
-constexpr int SEL_CAP = 10;       // 3 words per (d2, index) entry -> 30 <= HSTRIDE
+// (d2, traversal); here by (d2, sorted index)), one lane per point, no cross-lane traffic.
+//
+// The neighbours are ranked by the key (d2, k). A selection state splits the ball into
+// "below" (certainly among the max_nn nearest), "members" (still undecided) and "above":
+//   * an interval [dlo, dhi] x [klo, khi] of keys holding the members of the previous level
+//     (exact: it is the min/max over them, and a monotone classification's member set is
+//     exactly the keys between its extremes);
+//   * a current level that bins the members, by d2 or -- once they all share one d2 -- by k:
+//     bin(v) = clamp(floor((v - lo) * scale), 0, nb - 1), monotone in v (IEEE subtraction and
+//     multiplication by a positive constant are monotone), and the chosen bin b.
+// Every scan re-evaluates the same functions, so the classification is bit-for-bit consistent.
+//   scan 1: count + centred cumulants of the ball and, when the ball's cells hold more than
+//           max_nn points, the level-0 histogram (128 u8 bins of d2 over [0, r^2)) in the
+//           lane's own LDS row. count <= max_nn (two thirds of the points): done.
+//   else:   choose the bin holding the max_nn-th neighbour. A planar patch is uniform in d2, so
+//           it holds ~5 points and usually fits SEL_CAP at once; otherwise rescan the ball of
+//           radius sqrt(top) for the members' extremes and a 32-bin u32 histogram of them
+//           (also the restart when a u8 bin saturates); exact d2 ties go on by index.
+//   final:  rescan, accumulate every point below, collect the members (<= SEL_CAP) in the LDS
+//           row and add the `need` smallest by (d2, k).
+constexpr int NB8 = 128;          // level-0 bins (u8 counters)
+constexpr int NB32 = 32;          // refinement bins (u32 counters)
+constexpr int HSTRIDE = 33;       // LDS words per lane: 128 u8 / 32 u32 bins, padded to odd
+constexpr int SEL_CAP = 11;       // 3 words per (d2, index) entry -> 33 <= HSTRIDE
+constexpr int MAX_REFINE = 32;    // d2 levels (~11 x 5 bits) then index levels (<= 7 x 5 bits)
 
 // search radius covering every point with d2 < hi (slack for the f32 cell arithmetic)
 __device__ __forceinline__ float sel_radius(double hi, float r) {
     return fminf(float(sqrt(hi)) * 1.0001f + 1e-5f, r);
 }
 
-__device__ __forceinline__ double sel_bound(double lo, double hi, double width, int b) {
-    return b <= 0 ? lo : (b >= NB ? hi : lo + width * double(b));
+struct Sel {
+    double dlo, dhi;       // member interval in d2 (inclusive)
+    uint32_t klo, khi;     // member interval in k (inclusive)
+    double lo, scale;      // current level: bins of d2 (by_idx = 0) or of k (by_idx = 1)
+    int nb, b, by_idx;
+};
+
+__device__ __forceinline__ int sel_level_bin(const Sel &S, double d2, uint32_t k) {
+    const double v = S.by_idx ? double(k) : d2;
+    const double t = (v - S.lo) * S.scale;
+    return t < 0.0 ? 0 : (t >= double(S.nb) ? S.nb - 1 : int(t));
 }
 
-__device__ __forceinline__ int sel_bin(double d2, double lo, double hi, double width, double scale) {
-    int b = (int)((d2 - lo) * scale);
-    b = b < 0 ? 0 : (b >= NB ? NB - 1 : b);
-    while (b > 0 && d2 < sel_bound(lo, hi, width, b)) --b;
-    while (b < NB - 1 && d2 >= sel_bound(lo, hi, width, b + 1)) ++b;
-    return b;
+// -1: below (certainly among the max_nn nearest), 0: member, 1: above
+__device__ __forceinline__ int sel_classify(const Sel &S, double d2, uint32_t k) {
+    if (d2 < S.dlo) return -1;
+    if (d2 > S.dhi) return 1;
+    if (k < S.klo) return -1;
+    if (k > S.khi) return 1;
+    const int b = sel_level_bin(S, d2, k);
+    return b < S.b ? -1 : (b > S.b ? 1 : 0);
 }
 
 __global__ void __launch_bounds__(PT_THREADS)
 normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *stats) {
     __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
     uint32_t *H = lds + threadIdx.x * HSTRIDE;
+    uint8_t *H8 = reinterpret_cast<uint8_t *>(H);
     const Seg s = segs[blockIdx.x];
     const CloudDev C = cd[s.cloud];
     const int j = s.start + threadIdx.x;
     if (j >= C.n) return;
-    const float4 qf = C.xyz[j];
+    const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
+    float4 *nrm = const_cast<float4 *>(C.nrm);
     // candidates in the ball's cells: when they cannot exceed max_nn, no selection is needed
     uint32_t box = 0;
-    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b) { box += b - a; });
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float, float) { box += b - a; });
     const bool hist = box > uint32_t(np.max_nn);
     if (hist) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) H[b] = 0;
+        for (int b = 0; b < NB8 / 4; ++b) H[b] = 0;
     }
-    double lo = 0.0, hi = np.r2;
-    double width = (hi - lo) / double(NB), scale = double(NB) / (hi - lo);
+    Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
+    bool sat = false;
     Cum c = {};
-    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b) {
-        for (uint32_t k = a; k < b; ++k) {
-            const float4 p = C.xyz[k];
-            double d2;
-            if (in_ball(np, qf, qx, qy, qz, p, d2)) {
-                cum_add(c, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
-                if (hist) H[sel_bin(d2, lo, hi, width, scale)] += 1;
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+        scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+            Off o;
+            if (in_ball(np, qf, qx, qy, qz, p, o)) {
+                cum_add(c, o);
+                if (hist) {
+                    const int bb = sel_level_bin(S, o.d2, k);
+                    const uint32_t v = H8[bb];
+                    if (v == 255u) sat = true;
+                    else H8[bb] = uint8_t(v + 1u);
+                }
             }
-        }
+        });
     });
-    float4 *nrm = const_cast<float4 *>(C.nrm);
     if (c.n <= np.max_nn) {
         nrm[j] = normal_from_cum(c);
         return;
     }
     if (stats) atomicAdd(stats, 1u);
-    uint32_t need = uint32_t(np.max_nn);   // still to take from [lo, hi)
-    for (int it = 0; it < 8; ++it) {
+    double top = np.r2;   // every point below or member has d2 <= top (up to rounding)
+    // rescan the members of the current state: their key extremes and a histogram by `next`
+    auto refine = [&](const Sel &next, double &dmin, double &dmax, uint32_t &kmin, uint32_t &kmax) {
+#pragma unroll
+        for (int b = 0; b < NB32; ++b) H[b] = 0;
+        dmin = INFINITY;
+        dmax = -INFINITY;
+        kmin = 0xffffffffu;
+        kmax = 0u;
+        ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
+            scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+                Off o;
+                if (in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
+                    H[sel_level_bin(next, o.d2, k)] += 1;
+                    dmin = fmin(dmin, o.d2);
+                    dmax = fmax(dmax, o.d2);
+                    kmin = min(kmin, k);
+                    kmax = max(kmax, k);
+                }
+            });
+        });
+    };
+    uint32_t need = uint32_t(np.max_nn);   // still to take from the members
+    bool u8 = true;
+    if (sat) {                             // a u8 bin saturated: level 0 as 32 x u32 bins
+        Sel next = S;
+        next.scale = double(NB32) / np.r2;
+        next.nb = NB32;
+        S.b = 0;
+        S.scale = 0.0;                     // every ball point is a member (one bin)
+        S.nb = 1;
+        double dmin, dmax;
+        uint32_t kmin, kmax;
+        refine(next, dmin, dmax, kmin, kmax);
+        S = next;
+        u8 = false;
+    }
+    for (int it = 0; it < MAX_REFINE; ++it) {
         uint32_t acc = 0;
-        int bstar = NB - 1;
-        for (int b = 0; b < NB; ++b) {
-            if (acc + H[b] >= need) {
+        int bstar = S.nb - 1;
+        for (int b = 0; b < S.nb; ++b) {
+            const uint32_t hb = u8 ? uint32_t(H8[b]) : H[b];
+            if (acc + hb >= need) {
                 bstar = b;
                 break;
             }
-            acc += H[b];
+            acc += hb;
         }
-        const uint32_t bin_count = H[bstar];
+        const uint32_t bin_count = u8 ? uint32_t(H8[bstar]) : H[bstar];
         need -= acc;
-        const double nlo = sel_bound(lo, hi, width, bstar), nhi = sel_bound(lo, hi, width, bstar + 1);
-        lo = nlo;
-        hi = nhi;
-        if (bin_count <= SEL_CAP || !(hi > lo)) break;
-        width = (hi - lo) / double(NB);
-        scale = double(NB) / (hi - lo);
-#pragma unroll
-        for (int b = 0; b < NB; ++b) H[b] = 0;
-        // only d2 < hi matters from here on: scan the smaller ball of radius sqrt(hi)
-        ball_visit_runs(C, qf, sel_radius(hi, np.r), [&](uint32_t a, uint32_t b) {
-            for (uint32_t k = a; k < b; ++k) {
-                const float4 p = C.xyz[k];
-                double d2;
-                if (in_ball(np, qf, qx, qy, qz, p, d2) && d2 >= lo && d2 < hi)
-                    H[sel_bin(d2, lo, hi, width, scale)] += 1;
-            }
-        });
+        S.b = bstar;
+        if (!S.by_idx) top = fmin(top, S.lo + double(bstar + 1) / S.scale);
+        if (bin_count <= SEL_CAP) break;
+        // next level over the chosen bin's range, clipped to the exact member extremes known
+        // so far (so no member falls below lo: a clamped lowest bin could never split); the
+        // extremes found by the same scan then replace the whole classification chain
+        Sel next = S;
+        {
+            const double vlo = S.by_idx ? double(S.klo) : S.dlo;
+            const double vhi = S.by_idx ? double(S.khi) + 1.0 : S.dhi;
+            const double elo = fmax(S.lo + double(bstar) / S.scale, vlo);
+            const double ehi = fmin(S.lo + double(bstar + 1) / S.scale, vhi);
+            next.lo = elo;
+            next.scale = ehi > elo ? double(NB32) / (ehi - elo) : S.scale * double(NB32);
+            next.nb = NB32;
+        }
+        double dmin, dmax;
+        uint32_t kmin, kmax;
+        refine(next, dmin, dmax, kmin, kmax);
+        u8 = false;
+        if (!S.by_idx && dmin == dmax) {
+            // every member has the same d2: order them by index instead
+            next.by_idx = 1;
+            next.lo = double(kmin);
+            next.scale = double(NB32) / (double(kmax - kmin) + 1.0);
+            refine(next, dmin, dmax, kmin, kmax);
+        }
+        next.dlo = dmin;
+        next.dhi = dmax;
+        next.klo = next.by_idx ? kmin : 0u;
+        next.khi = next.by_idx ? kmax : 0xffffffffu;
+        top = fmin(top, dmax);
+        S = next;
     }
-    // final pass: everything below lo, plus the `need` smallest members of [lo, hi)
+    // final pass: everything below, plus the `need` smallest members
     Cum f = {};
     uint32_t m = 0;
-    ball_visit_runs(C, qf, sel_radius(hi, np.r), [&](uint32_t a, uint32_t b) {
-        for (uint32_t k = a; k < b; ++k) {
-            const float4 p = C.xyz[k];
-            double d2;
-            if (!in_ball(np, qf, qx, qy, qz, p, d2)) continue;
-            if (d2 < lo) {
-                cum_add(f, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
-            } else if (d2 < hi) {
+    ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
+        scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+            Off o;
+            if (!in_ball(np, qf, qx, qy, qz, p, o)) return;
+            const int cl = sel_classify(S, o.d2, k);
+            if (cl < 0) {
+                cum_add(f, o);
+            } else if (cl == 0) {
                 if (m < SEL_CAP) {
-                    const uint64_t bits = __double_as_longlong(d2);
+                    const uint64_t bits = __double_as_longlong(o.d2);
                     H[3 * m] = uint32_t(bits);
                     H[3 * m + 1] = uint32_t(bits >> 32);
                     H[3 * m + 2] = k;
                 }
                 ++m;
             }
-        }
+        });
     });
     const uint32_t mm = m < SEL_CAP ? m : SEL_CAP;
     for (uint32_t e = 0; e < mm; ++e) {
@@ -558,10 +690,7 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *s
             // positive doubles order like their bit patterns
             rank += (bg < be || (bg == be && H[3 * g + 2] < ke)) ? 1u : 0u;
         }
-        if (rank < need) {
-            const float4 p = C.xyz[ke];
-            cum_add(f, (double)p.x - qx, (double)p.y - qy, (double)p.z - qz);
-        }
+        if (rank < need) cum_add(f, make_off(lsm_ld(C.xyz, ke), qx, qy, qz));
     }
     nrm[j] = normal_from_cum(f);
 }

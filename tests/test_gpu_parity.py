@@ -105,6 +105,44 @@ def test_normals(dev, seq8k, seq64k, which):
         _release(dev, ids)
 
 
+def test_normals_degenerate_neighbourhoods(dev):
+    """kNN-300 truncation on pathological neighbourhoods: 400 exact duplicates of one point (one
+    d2 value holds more than a u8 histogram bin can count and more than the selection buffer
+    can rank, so the u32 restart and the tie cap both run), a dense planar patch, and points
+    whose neighbours sit at exactly equal distances (a regular grid). Ties at one distance are
+    ties between identical contributions (duplicates) or symmetric ones, so the normal is
+    determined; it must match the oracle."""
+    rng = np.random.default_rng(7)
+    patch = np.c_[5.0 + rng.uniform(-0.2, 0.2, 1500), rng.uniform(-0.2, 0.2, 1500),
+                  0.002 * rng.standard_normal(1500)]
+    dup = np.repeat([[5.05, 0.03, 0.0]], 400, axis=0)
+    g = np.arange(-10, 11) * 0.02
+    gx, gy = np.meshgrid(g, g)
+    grid = np.c_[8.0 + gx.ravel(), 1.0 + gy.ravel(), 0.5 + 0.0 * gx.ravel()]
+    wall = np.c_[np.full(900, 12.0) + 0.001 * rng.standard_normal(900),
+                 rng.uniform(-0.3, 0.3, 900), rng.uniform(0.0, 0.6, 900)]
+    cloud = np.vstack([patch, dup, grid, wall]).astype(np.float32)
+    ids = _prep(dev, [cloud])
+    try:
+        xyz, nrm = dev.download(ids[0], normals=True)
+        ref_pts = O.filter_radius_height(cloud)
+        assert np.array_equal(xyz, ref_pts)
+        ref_n, counts = O.estimate_normals(ref_pts, return_counts=True)
+        assert (counts >= 300).sum() > 1000
+        # a patch point next to the duplicates can keep itself + 299 copies: a rank-1
+        # covariance whose normal is any vector of a plane (not determined) -- skip those
+        from scipy.spatial import cKDTree
+        p64 = ref_pts.astype(np.float64)
+        idx, _, cnt = O.hybrid_search(cKDTree(p64), p64, p64, 0.3, 300)
+        ev = np.linalg.eigvalsh(O.compute_covariance(p64, idx, cnt))
+        determined = (ev[:, 1] - ev[:, 0]) > 1e-6 * np.maximum(ev[:, 2], 1e-30)
+        assert determined.mean() > 0.99
+        d = _normal_agreement(nrm, ref_n)
+        assert (d[determined] > 1.0 - 1e-5).all(), np.sort(d[determined])[:10]
+    finally:
+        _release(dev, ids)
+
+
 # ------------------------------------------------------------------ ICP (a6)
 def _oracle_pair(seq, i, method, max_iteration=30):
     tgt = O.filter_radius_height(seq.scans[i])
