@@ -166,9 +166,7 @@ def main():
             "cpu_baseline": cpu,
             "mean_icp_iterations": float(np.mean(iters)),
             "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
-                                      for k, v in stats.items() if v["launches"]},
-            "nn_lds_staged_fraction": round(dev.kernel_stats("nn_staged_blocks")["launches"] /
-                                            max(dev.kernel_stats("nn_blocks")["launches"], 1), 4),
+                                      for k, v in stats.items() if v["launches"]}
         }
         print(json.dumps(out), flush=True)
     if group is not None:

@@ -71,40 +71,56 @@ __device__ __forceinline__ void try_point(const float4 t, uint32_t k, float qx, 
     }
 }
 
-// Points of a cell are sorted by x (grid build). Small cells are scanned whole; larger ones are
-// entered at the query's x by binary search and walked outwards until dx^2 exceeds the best
-// squared distance (a point with dx^2 > best cannot be nearer; equality is still examined so
-// (d2, index) ties resolve exactly as a full scan would).
-__device__ __forceinline__ void scan_run(const float4 *__restrict__ xyz, uint32_t a, uint32_t b,
-                                         float qx, float qy, float qz, float &bd2, int &bidx) {
-    if (b - a <= 8) {
-        for (uint32_t k = a; k < b; ++k) try_point(xyz[k], k, qx, qy, qz, bd2, bidx);
+// One x-sorted run [a, b) of a cell row whose slab is at least dyz2 (squared, underestimated)
+// from the query: enter at the query's x (binary search on long runs) and walk outwards while
+// dx^2 + dyz2 <= best (strict '>' stops: equal distances are still examined, so (d2, index)
+// ties resolve exactly as a full scan would).
+constexpr uint32_t NN_LINEAR = 8;
+
+__device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float qx,
+                                         float qy, float qz, float dyz2, float &bd2, int &bidx) {
+    if (b - a <= NN_LINEAR) {
+        for (uint32_t k = a; k < b; ++k) try_point(lsm_ld(xyz, k), k, qx, qy, qz, bd2, bidx);
         return;
     }
+    const float *xs = reinterpret_cast<const float *>(xyz);
     uint32_t lo = a, hi = b;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (xyz[mid].x < qx) lo = mid + 1;
+        if (lsm_ld(xs, size_t(mid) * 4) < qx) lo = mid + 1;
         else hi = mid;
     }
     for (uint32_t k = lo; k < b; ++k) {
-        const float4 t = xyz[k];
+        const float4 t = lsm_ld(xyz, k);
         const float dx = t.x - qx;
-        if (dx * dx > bd2) break;
+        if (dx * dx + dyz2 > bd2) break;
         try_point(t, k, qx, qy, qz, bd2, bidx);
     }
     for (uint32_t k = lo; k > a;) {
         --k;
-        const float4 t = xyz[k];
+        const float4 t = lsm_ld(xyz, k);
         const float dx = qx - t.x;
-        if (dx * dx > bd2) break;
+        if (dx * dx + dyz2 > bd2) break;
         try_point(t, k, qx, qy, qz, bd2, bidx);
     }
+}
+
+// squared distance (in cells^2) from fractional coordinate f to cell k's slab [k, k+1)
+__device__ __forceinline__ float slab_cells2(float f, int k) {
+    const float d = f < float(k) ? float(k) - f : (f > float(k + 1) ? f - float(k + 1) : 0.f);
+    return d * d;
 }
 
 // ------------------------------------------------------------------------------------------
 // correspondence search (the hot kernel)
 // ------------------------------------------------------------------------------------------
+// Search box: the cells within the warm-start radius R = sqrt(previous neighbour's distance)
+// (at most NN_KMAX cells each way), or the 3x3x3 block around the query's cell on a cold start.
+// Rows of cells are visited centre-out and pruned by their slab distance; inside a row the
+// x-sorted runs are walked from the query's x. A query is resolved when its best distance is
+// provably below every unsearched point (the box faces not clipped by the grid), else queued.
+constexpr int NN_KMAX = 4;
+
 __global__ void __launch_bounds__(NN_THREADS)
 nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
           const CloudDev *__restrict__ cds, NNParams prm, int32_t *__restrict__ corr,
@@ -124,13 +140,13 @@ nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
     bool pending = false;
     if (live) {
         double qx64, qy64, qz64;
-        transform_point(P.T, S.xyz[i], qx64, qy64, qz64);
+        transform_point(P.T, lsm_ld(S.xyz, i), qx64, qy64, qz64);
         const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
         // warm start: the previous pass's nearest neighbour bounds this pass's search. The search
         // stays exact -- the (d2, index) minimum over all points does not depend on the start.
         const int prev = corr[P.src_off + i];
         if (prev >= 0 && prev < G.n) {
-            const float4 t = G.xyz[prev];
+            const float4 t = lsm_ld(G.xyz, prev);
             const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
             bd2 = dx * dx + dy * dy + dz * dz;
             bidx = prev;
@@ -143,47 +159,56 @@ nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
         if (!inside) {
             pending = G.n > 0;   // outside the target's box: let the fallback decide
         } else {
-            const float ax = fx - cx, ay = fy - cy, az = fz - cz;
-            const float c2s = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
-            // squared distance (in cells^2) from q to the neighbour slab on each side
-            const float lx = ax * ax, hx = (1.f - ax) * (1.f - ax);
-            const float ly = ay * ay, hy = (1.f - ay) * (1.f - ay);
-            const float lz = az * az, hz = (1.f - az) * (1.f - az);
-            const uint32_t *cs = G.cell_start;
-            // own cell first
-            {
-                const int lin = lsm_cell_lin(G.nbx, G.nby, cx, cy, cz);
-                scan_run(G.xyz, cs[lin], cs[lin + 1], qx, qy, qz, bd2, bidx);
+            // box half-width in cells: the warm-start radius (+ f32 slack), else one cell
+            int K = 1;
+            if (bd2 < INFINITY) {
+                const float rc = sqrtf(bd2) * G.inv_cell * 1.0001f + 1e-4f;
+                K = rc >= float(NN_KMAX) ? NN_KMAX : max(1, (int)ceilf(rc));
             }
+            const int x0 = max(cx - K, 0), x1 = min(cx + K, G.nx - 1);
+            const int y0 = max(cy - K, 0), y1 = min(cy + K, G.ny - 1);
+            const int z0 = max(cz - K, 0), z1 = min(cz + K, G.nz - 1);
+            const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
+            const uint32_t *cs = G.cell_start;
 #pragma unroll 1
-            for (int dz = -1; dz <= 1; ++dz) {
+            for (int iz = 0; iz <= 2 * K; ++iz) {
+                const int dz = (iz & 1) ? -((iz + 1) >> 1) : (iz >> 1);   // 0, -1, 1, -2, 2 ...
                 const int z = cz + dz;
-                if (z < 0 || z >= G.nz) continue;
-                const float wz = (dz < 0 ? lz : (dz > 0 ? hz : 0.f)) * c2s;
+                if (z < z0 || z > z1) continue;
+                const float wz = slab_cells2(fz, z) * c2;
                 if (wz >= bd2) continue;
 #pragma unroll 1
-                for (int dy = -1; dy <= 1; ++dy) {
+                for (int iy = 0; iy <= 2 * K; ++iy) {
+                    const int dy = (iy & 1) ? -((iy + 1) >> 1) : (iy >> 1);
                     const int y = cy + dy;
-                    if (y < 0 || y >= G.ny) continue;
-                    const float wyz = wz + (dy < 0 ? ly : (dy > 0 ? hy : 0.f)) * c2s;
+                    if (y < y0 || y > y1) continue;
+                    const float wyz = wz + slab_cells2(fy, y) * c2;
                     if (wyz >= bd2) continue;
-#pragma unroll 1
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        if ((dx | dy | dz) == 0) continue;
-                        const int x = cx + dx;
-                        if (x < 0 || x >= G.nx) continue;
-                        const float w = wyz + (dx < 0 ? lx : (dx > 0 ? hx : 0.f)) * c2s;
-                        if (w >= bd2) continue;
-                        const int lin = lsm_cell_lin(G.nbx, G.nby, x, y, z);
-                        scan_run(G.xyz, cs[lin], cs[lin + 1], qx, qy, qz, bd2, bidx);
+                    // cells of this row that can still hold a point nearer than the best
+                    int xa = x0, xb = x1;
+                    if (bd2 < INFINITY) {
+                        const float ch = sqrtf((bd2 - wyz) * 1.0002f) * G.inv_cell + 1e-4f;
+                        xa = max(xa, (int)floorf(fx - ch));
+                        xb = min(xb, (int)floorf(fx + ch));
+                    }
+                    int x = xa;
+                    while (x <= xb) {
+                        const int xe = min(xb, x | (LSM_BLK - 1));   // end of this block's row part
+                        const uint32_t a = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, x, y, z));
+                        const uint32_t b = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, xe, y, z) + 1);
+                        if (b > a) scan_run(G.xyz, a, b, qx, qy, qz, wyz, bd2, bidx);
+                        x = xe + 1;
                     }
                 }
             }
-            // every point outside the 3x3x3 block is at least `bound` away (in cells); sides
-            // clipped by the grid hold no points.
-            float bx = fminf(cx >= 2 ? ax + 1.f : INFINITY, cx + 2 < G.nx ? 2.f - ax : INFINITY);
-            float by = fminf(cy >= 2 ? ay + 1.f : INFINITY, cy + 2 < G.ny ? 2.f - ay : INFINITY);
-            float bz = fminf(cz >= 2 ? az + 1.f : INFINITY, cz + 2 < G.nz ? 2.f - az : INFINITY);
+            // every point outside the searched box is at least `bound` away; sides clipped by
+            // the grid hold no points.
+            const float bx = fminf(cx - K > 0 ? fx - float(cx - K) : INFINITY,
+                                   cx + K + 1 < G.nx ? float(cx + K + 1) - fx : INFINITY);
+            const float by = fminf(cy - K > 0 ? fy - float(cy - K) : INFINITY,
+                                   cy + K + 1 < G.ny ? float(cy + K + 1) - fy : INFINITY);
+            const float bz = fminf(cz - K > 0 ? fz - float(cz - K) : INFINITY,
+                                   cz + K + 1 < G.nz ? float(cz + K + 1) - fz : INFINITY);
             const float bound = fminf(bx, fminf(by, bz)) * G.cell;
             const float bound2 = bound * bound * 0.99999f;
             if (bd2 <= bound2 || bound >= prm.maxc) {
@@ -278,7 +303,7 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
         const CloudDev S = cds[P.src];
         const CloudDev G = cds[P.tgt];
         double qx64, qy64, qz64;
-        transform_point(P.T, S.xyz[q.i], qx64, qy64, qz64);
+        transform_point(P.T, lsm_ld(S.xyz, q.i), qx64, qy64, qz64);
         const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
         float bd2 = q.best_d2;
         int bidx = q.best;
@@ -309,8 +334,8 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
                                               gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
                             if (lb2 * 0.9999f < bd2) {
                                 const int bid = (bz * G.nby + by) * G.nbx + bx;
-                                a = cs[bid * LSM_BLK_CELLS];
-                                b = cs[(bid + 1) * LSM_BLK_CELLS];
+                                a = lsm_ld(cs, size_t(bid) * LSM_BLK_CELLS);
+                                b = lsm_ld(cs, size_t(bid + 1) * LSM_BLK_CELLS);
                             }
                         }
                     }
@@ -320,7 +345,7 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
                         mask &= mask - 1;
                         const uint32_t ra = __shfl(a, src, LSM_WAVE), rb = __shfl(b, src, LSM_WAVE);
                         for (uint32_t k = ra + lane; k < rb; k += LSM_WAVE) {
-                            const float4 t4 = G.xyz[k];
+                            const float4 t4 = lsm_ld(G.xyz, k);
                             const float ex = qx - t4.x, ey = qy - t4.y, ez = qz - t4.z;
                             const float d2 = ex * ex + ey * ey + ez * ez;
                             if (better(d2, int(k), bd2, bidx)) {
@@ -373,14 +398,14 @@ accumulate_kernel(const BlockTask *__restrict__ tasks, const PairState *__restri
         const int idx = corr[P.src_off + i];
         if (idx >= 0) {
             double x, y, z;
-            transform_point(P.T, S.xyz[i], x, y, z);
-            const float4 t = G.xyz[idx];
+            transform_point(P.T, lsm_ld(S.xyz, i), x, y, z);
+            const float4 t = lsm_ld(G.xyz, idx);
             const double tx = t.x, ty = t.y, tz = t.z;
             const double ex = x - tx, ey = y - ty, ez = z - tz;
             acc[28] = (ex * ex + ey * ey) + ez * ez;
             acc[29] = 1.0;
             if (METHOD == LSM_P2PLANE) {
-                const float4 nf = G.nrm[idx];
+                const float4 nf = lsm_ld(G.nrm, idx);
                 const double nx = nf.x, ny = nf.y, nz = nf.z;
                 const double r = (ex * nx + ey * ny) + ez * nz;
                 const double J[6] = {y * nz - z * ny, z * nx - x * nz, x * ny - y * nx, nx, ny, nz};
