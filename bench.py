@@ -166,7 +166,12 @@ def main():
             "cpu_baseline": cpu,
             "mean_icp_iterations": float(np.mean(iters)),
             "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
-                                      for k, v in stats.items() if v["launches"]}
+                                      for k, v in stats.items() if v["launches"]},
+            "nn_fallback_fraction": {
+                "all_passes": round(dev.kernel_stats("nn_pending")["launches"] /
+                                    max(dev.kernel_stats("nn_queries")["launches"], 1), 5),
+                "first_pass": round(dev.kernel_stats("nn_pending_first_pass")["launches"] /
+                                    max(dev.kernel_stats("nn_queries_first_pass")["launches"], 1), 5)}
         }
         print(json.dumps(out), flush=True)
     if group is not None:

@@ -120,6 +120,7 @@ __device__ __forceinline__ float slab_cells2(float f, int k) {
 // x-sorted runs are walked from the query's x. A query is resolved when its best distance is
 // provably below every unsearched point (the box faces not clipped by the grid), else queued.
 constexpr int NN_KMAX = 4;
+constexpr int NN_KCOLD = 2;   // cold start (no previous neighbour): 5x5x5 cells
 
 __global__ void __launch_bounds__(NN_THREADS)
 nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
@@ -153,14 +154,13 @@ nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
         }
         const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
                     fz = (qz - G.oz) * G.inv_cell;
-        const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
-        const bool inside = G.n > 0 && cx >= 0 && cx < G.nx && cy >= 0 && cy < G.ny && cz >= 0 &&
-                            cz < G.nz;
-        if (!inside) {
-            pending = G.n > 0;   // outside the target's box: let the fallback decide
-        } else {
-            // box half-width in cells: the warm-start radius (+ f32 slack), else one cell
-            int K = 1;
+        // a query outside the target's box searches around the nearest cell of the box: the
+        // box faces that lie on the grid boundary bound nothing (no points beyond them)
+        auto clampc = [](float f, int n) { return (int)fminf(fmaxf(floorf(f), 0.f), float(n - 1)); };
+        const int cx = clampc(fx, G.nx), cy = clampc(fy, G.ny), cz = clampc(fz, G.nz);
+        if (G.n > 0) {
+            // box half-width in cells: the warm-start radius (+ f32 slack), else NN_KCOLD
+            int K = NN_KCOLD;
             if (bd2 < INFINITY) {
                 const float rc = sqrtf(bd2) * G.inv_cell * 1.0001f + 1e-4f;
                 K = rc >= float(NN_KMAX) ? NN_KMAX : max(1, (int)ceilf(rc));
@@ -850,8 +850,18 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
     int64_t nactive = npairs;
     std::vector<int32_t> hflags(npairs);
+    int passes = 0;
+    int64_t queries = 0, queries0 = 0;   // source points searched (all passes / first pass)
     for (int pass = 0; pass <= max_iter && ntasks > 0; ++pass) {
         hipEvent_t ev;
+        ++passes;
+        if (ctx->timing) {
+            int64_t qn = 0;
+            for (int64_t k = 0; k < npairs; ++k)
+                if (act[k]) qn += ps[k].nsrc;
+            queries += qn;
+            if (pass == 0) queries0 = qn;
+        }
         ctx->tic("nn", &ev);
         nn_kernel<<<ntasks, NN_THREADS, 0, st>>>(d_tasks, d_ps, d_cd, prm, d_corr, d_cd2, d_q,
                                                  d_qn + pass, qcap);
@@ -922,7 +932,18 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
     }
     ctx->collect_timings();
-    if (ctx->timing) ctx->stats["nn"].algo_bytes += nn_bytes;
+    if (ctx->timing) {
+        ctx->stats["nn"].algo_bytes += nn_bytes;
+        // search statistics: queries and the ones the fast path left to the fallback
+        std::vector<uint32_t> qn(passes);
+        LSM_HIP_TRY(ctx, hipMemcpy(qn.data(), d_qn, size_t(passes) * 4, hipMemcpyDeviceToHost));
+        int64_t pend = 0;
+        for (int k = 0; k < passes; ++k) pend += qn[k];
+        ctx->stats["nn_queries"].launches += queries;
+        ctx->stats["nn_queries_first_pass"].launches += queries0;
+        ctx->stats["nn_pending"].launches += pend;
+        ctx->stats["nn_pending_first_pass"].launches += passes > 0 ? qn[0] : 0;
+    }
     for (int64_t k = 0; k < npairs; ++k) {
         const PairState &P = ps[k];
         lsm_icp_result &R = out[k];
