@@ -12,7 +12,8 @@ import threading
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "liblidarsm.so")
+LIB_PATH = os.environ.get("LIDARSM_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "_lib", "liblidarsm.so")   # env: A/B builds
 
 LSM_OK = 0
 LSM_P2P = 0

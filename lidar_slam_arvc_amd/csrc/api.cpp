@@ -386,6 +386,23 @@ int lsm_icp(lsm_ctx *ctx, lsm_cloud src, lsm_cloud tgt, const double init[16],
 
 int lsm_icp_last_correspondences(lsm_ctx *ctx, int64_t *pairs, int64_t cap, int64_t *n) {
     if (!ctx || !n) return LSM_EINVAL;
+    if (ctx->last_corr_pending) {   // compact the dense device array (source reference order)
+        const int64_t n0 = ctx->last_corr_dense_n;
+        std::vector<int32_t> dense(size_t(std::max<int64_t>(n0, 0)));
+        if (n0 > 0) {
+            void *d = ctx->buf("i_lastcorr_dense", size_t(n0) * 4);
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(dense.data(), d, size_t(n0) * 4, hipMemcpyDeviceToHost,
+                                            ctx->stream));
+            LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        ctx->last_corr.clear();
+        for (int64_t i = 0; i < n0; ++i)
+            if (dense[size_t(i)] >= 0) {
+                ctx->last_corr.push_back(i);
+                ctx->last_corr.push_back(dense[size_t(i)]);
+            }
+        ctx->last_corr_pending = false;
+    }
     int64_t m = int64_t(ctx->last_corr.size() / 2);
     *n = m;
     if (pairs) {

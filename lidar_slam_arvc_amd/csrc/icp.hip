@@ -112,6 +112,77 @@ __device__ __forceinline__ float slab_cells2(float f, int k) {
 }
 
 // ------------------------------------------------------------------------------------------
+// device-side work plan: the blocks of the pairs still iterating, balanced over the XCDs
+// ------------------------------------------------------------------------------------------
+// Logical block g (pair order, active pairs only) lives in XCD lane l = g / per at position
+// m = g % per; grid slot t = 8 m + l, so consecutive workgroups (round-robin over the 8 XCDs)
+// take one lane each: a pair stays on one or two XCDs (its target stays in those L2s) and a
+// lone straggler pair still spreads over the whole chip. Rebuilt on the device after every
+// solve, so the host never waits between passes.
+struct TaskPlan {
+    const int32_t *plan;   // [0] active blocks, [1] per-lane blocks
+    const int32_t *pref;   // [npairs + 1] prefix of the active pairs' block counts
+    int npairs;
+};
+
+constexpr int PLAN_THREADS = 1024;
+
+__global__ void __launch_bounds__(PLAN_THREADS)
+plan_kernel(const PairState *__restrict__ st, int npairs, int32_t *__restrict__ pref,
+            int32_t *__restrict__ plan) {
+    __shared__ int32_t wsum[PLAN_THREADS / LSM_WAVE];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int32_t carry = 0;
+    for (int base = 0; base < npairs; base += PLAN_THREADS) {
+        const int k = base + threadIdx.x;
+        const int32_t v = (k < npairs && st[k].active) ? st[k].nblk : 0;
+        int32_t x = v;   // inclusive wave scan
+#pragma unroll
+        for (int off = 1; off < LSM_WAVE; off <<= 1) {
+            const int32_t y = __shfl_up(x, off, LSM_WAVE);
+            if (lane >= off) x += y;
+        }
+        if (lane == LSM_WAVE - 1) wsum[w] = x;
+        __syncthreads();
+        int32_t before = carry, tot = 0;
+        for (int q = 0; q < PLAN_THREADS / LSM_WAVE; ++q) {
+            before += q < w ? wsum[q] : 0;
+            tot += wsum[q];
+        }
+        if (k < npairs) pref[k + 1] = before + x;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        pref[0] = 0;
+        plan[0] = carry;
+        plan[1] = (carry + NXCD - 1) / NXCD;
+    }
+}
+
+// grid slot t -> block task: 1 = work, 0 = padding, -1 = past the end of the plan
+__device__ __forceinline__ int plan_task(const TaskPlan &tp, const PairState *st, int t,
+                                         BlockTask &task) {
+    const int32_t total = tp.plan[0], per = tp.plan[1];
+    const int l = t & (NXCD - 1), m = t / NXCD;
+    if (m >= per) return -1;
+    const int32_t g = l * per + m;
+    if (g >= total) return 0;
+    int lo = 0, hi = tp.npairs;   // last pair with pref <= g (it has at least one block)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (lsm_ld(tp.pref, mid) <= g) lo = mid;
+        else hi = mid;
+    }
+    const int32_t blk = g - lsm_ld(tp.pref, lo);
+    task.pair = lo;
+    task.start = blk * NN_THREADS;
+    task.slot = st[lo].blk0 + blk;
+    task.pad = 0;
+    return 1;
+}
+
+// ------------------------------------------------------------------------------------------
 // correspondence search (the hot kernel)
 // ------------------------------------------------------------------------------------------
 // Search box: the cells within the warm-start radius R = sqrt(previous neighbour's distance)
@@ -122,13 +193,11 @@ __device__ __forceinline__ float slab_cells2(float f, int k) {
 constexpr int NN_KMAX = 4;
 constexpr int NN_KCOLD = 2;   // cold start (no previous neighbour): 5x5x5 cells
 
-__global__ void __launch_bounds__(NN_THREADS)
-nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
-          const CloudDev *__restrict__ cds, NNParams prm, int32_t *__restrict__ corr,
-          float *__restrict__ corr_d2, FallbackItem *__restrict__ queue,
-          uint32_t *__restrict__ queue_n, uint32_t queue_cap) {
-    const BlockTask task = tasks[blockIdx.x];
-    if (task.pair < 0) return;
+__device__ __forceinline__ void nn_task(const BlockTask task, const PairState *__restrict__ st,
+                                        const CloudDev *__restrict__ cds, const NNParams &prm,
+                                        int32_t *__restrict__ corr, float *__restrict__ corr_d2,
+                                        FallbackItem *__restrict__ queue,
+                                        uint32_t *__restrict__ queue_n, uint32_t queue_cap) {
     const PairState &P = st[task.pair];
     if (!P.active) return;
     const CloudDev S = cds[P.src];
@@ -234,6 +303,18 @@ nn_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
         const int64_t g = P.src_off + i;
         corr[g] = pending ? -2 : result;
         corr_d2[g] = bd2;
+    }
+}
+
+__global__ void __launch_bounds__(NN_THREADS)
+nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
+          NNParams prm, int32_t *__restrict__ corr, float *__restrict__ corr_d2,
+          FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n, uint32_t queue_cap) {
+    for (int t = blockIdx.x;; t += gridDim.x) {
+        BlockTask task;
+        const int r = plan_task(tp, st, t, task);
+        if (r < 0) break;
+        if (r > 0) nn_task(task, st, cds, prm, corr, corr_d2, queue, queue_n, queue_cap);
     }
 }
 
@@ -380,12 +461,11 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
 // residual / Jacobian accumulation (deterministic block partials)
 // ------------------------------------------------------------------------------------------
 template <int METHOD>
-__global__ void __launch_bounds__(NN_THREADS)
-accumulate_kernel(const BlockTask *__restrict__ tasks, const PairState *__restrict__ st,
-                  const CloudDev *__restrict__ cds, const int32_t *__restrict__ corr,
-                  double *__restrict__ partials) {
-    const BlockTask task = tasks[blockIdx.x];
-    if (task.pair < 0) return;
+__device__ __forceinline__ void accumulate_task(const BlockTask task,
+                                                const PairState *__restrict__ st,
+                                                const CloudDev *__restrict__ cds,
+                                                const int32_t *__restrict__ corr,
+                                                double *__restrict__ partials) {
     const PairState &P = st[task.pair];
     if (!P.active) return;
     const CloudDev S = cds[P.src];
@@ -445,6 +525,19 @@ accumulate_kernel(const BlockTask *__restrict__ tasks, const PairState *__restri
 #pragma unroll
         for (int q = 0; q < NN_THREADS / LSM_WAVE; ++q) s += red[q][threadIdx.x];
         partials[size_t(task.slot) * LSM_ACC + threadIdx.x] = s;
+    }
+}
+
+template <int METHOD>
+__global__ void __launch_bounds__(NN_THREADS)
+accumulate_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
+                  const int32_t *__restrict__ corr, double *__restrict__ partials) {
+    for (int t = blockIdx.x;; t += gridDim.x) {
+        BlockTask task;
+        const int r = plan_task(tp, st, t, task);
+        if (r < 0) break;
+        if (r > 0) accumulate_task<METHOD>(task, st, cds, corr, partials);
+        __syncthreads();   // the task's LDS reduction buffer is reused by the next task
     }
 }
 
@@ -607,7 +700,8 @@ __device__ void umeyama_update(const double *tot, double D[16]) {
 __global__ void __launch_bounds__(LSM_WAVE)
 solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NNParams prm,
              int pass, const double *__restrict__ pair_bytes, uint32_t *__restrict__ active_next,
-             double *__restrict__ bytes_next, int32_t *__restrict__ flags) {
+             double *__restrict__ bytes_next, unsigned long long *__restrict__ src_next,
+             int32_t *__restrict__ flags) {
     PairState &P = st[blockIdx.x];
     if (!P.active) return;
     __shared__ double tot[32];
@@ -678,18 +772,17 @@ solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NN
     P.prev_rmse = rmse;
     atomicAdd(active_next, 1u);
     atomicAdd(bytes_next, pair_bytes[blockIdx.x]);
+    atomicAdd(src_next, (unsigned long long)P.nsrc);
 }
 
-// copy a pair's final correspondences (reference order) for lsm_icp_last_correspondences
+// a pair's final correspondences as a dense array in reference order (for
+// lsm_icp_last_correspondences): dense[src_perm[i]] = tgt_perm[corr[i]] or -1
 __global__ void corr_to_ref(const int32_t *corr, int n, const uint32_t *src_perm,
-                            const uint32_t *tgt_perm, int64_t *out, uint32_t *count) {
+                            const uint32_t *tgt_perm, int32_t *dense) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int c = corr[i];
-    if (c < 0) return;
-    const uint32_t slot = atomicAdd(count, 1u);
-    out[2 * slot] = src_perm[i];
-    out[2 * slot + 1] = tgt_perm[c];
+    dense[src_perm[i]] = c >= 0 ? int32_t(tgt_perm[c]) : -1;
 }
 
 template <typename T>
@@ -770,50 +863,12 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                     double(tgt[k]->nonempty_cells) * 8.0 + double(nsrc) * 8.0;
         bytes0 += pbytes[k];
     }
-    auto build_tasks = [&](const std::vector<int32_t> &act) {
-        // fill the 8 XCD lanes in pair order, 1/8 of the blocks each: a pair stays on one or two
-        // XCDs (its target cloud stays in those L2s) and a lone straggler pair still spreads
-        // over the whole chip
-        std::vector<std::vector<BlockTask>> lanes(NXCD);
-        int64_t total = 0;
-        for (int64_t k = 0; k < npairs; ++k)
-            if (act[k]) total += ps[k].nblk;
-        const int64_t per = std::max<int64_t>((total + NXCD - 1) / NXCD, 1);
-        int l = 0;
-        int64_t filled = 0;
-        for (int64_t k = 0; k < npairs; ++k) {
-            if (!act[k]) continue;
-            const PairState &P = ps[k];
-            for (int b = 0; b < P.nblk; ++b) {
-                lanes[l].push_back({int32_t(k), b * NN_THREADS, P.blk0 + b, 0});
-                if (++filled == per && l < NXCD - 1) {
-                    ++l;
-                    filled = 0;
-                }
-            }
-        }
-        size_t maxlen = 0;
-        for (auto &l : lanes) maxlen = std::max(maxlen, l.size());
-        std::vector<BlockTask> t;
-        t.reserve(maxlen * NXCD);
-        for (size_t m = 0; m < maxlen; ++m)
-            for (int l = 0; l < NXCD; ++l)
-                t.push_back(m < lanes[l].size() ? lanes[l][m] : BlockTask{-1, 0, 0, 0});
-        while (!t.empty() && t.back().pair < 0) t.pop_back();
-        return t;
-    };
-    std::vector<int32_t> act(npairs, 1);
-    std::vector<BlockTask> tasks = build_tasks(act);
-    int ntasks = int(tasks.size());
     const int max_iter = p.max_iteration;
-
     CloudDev *d_cd;
     PairState *d_ps;
-    BlockTask *d_tasks;
     double *d_pbytes;
     if ((rc = upload(ctx, "i_cd", cdev, &d_cd))) return rc;
     if ((rc = upload(ctx, "i_ps", ps, &d_ps))) return rc;
-    if ((rc = upload(ctx, "i_tasks", tasks, &d_tasks))) return rc;
     if ((rc = upload(ctx, "i_pbytes", pbytes, &d_pbytes))) return rc;
     const size_t nsrc_tot = size_t(std::max<int64_t>(src_off, 1));
     int32_t *d_corr = (int32_t *)ctx->buf("i_corr", nsrc_tot * 4);
@@ -824,16 +879,20 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     const int ncnt = max_iter + 2;
     uint32_t *d_counters = (uint32_t *)ctx->buf("i_counters", size_t(ncnt) * 2 * 4);
     double *d_bytes = (double *)ctx->buf("i_bytes", size_t(ncnt) * 8);
-    if (!d_corr || !d_cd2 || !d_q || !d_part || !d_counters || !d_bytes) {
+    unsigned long long *d_srcn = (unsigned long long *)ctx->buf("i_srcn", size_t(ncnt) * 8);
+    int32_t *d_pref = (int32_t *)ctx->buf("i_pref", size_t(npairs + 1) * 4);
+    int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
+    int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
+    if (!d_corr || !d_cd2 || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
+        !d_plan || !d_flags) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
     }
     uint32_t *d_qn = d_counters;            // [ncnt] fallback queue sizes per pass
     uint32_t *d_active = d_counters + ncnt; // [ncnt] active pairs after each pass
-    int32_t *d_flags;
-    if ((rc = upload(ctx, "i_flags", act, &d_flags))) return rc;
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_counters, 0, size_t(ncnt) * 2 * 4, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_bytes, 0, size_t(ncnt) * 8, st));
+    LSM_HIP_TRY(ctx, hipMemsetAsync(d_srcn, 0, size_t(ncnt) * 8, st));
     if (src_off > 0) LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
 
     NNParams prm;
@@ -844,27 +903,43 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     prm.rel_fit = p.relative_fitness;
     prm.rel_rmse = p.relative_rmse;
 
-    uint32_t *h_active = (uint32_t *)ctx->host_pinned(64);
-    if (!h_active) return LSM_ENOMEM;
-    double nn_bytes = bytes0;
+    // Passes are launched back to back; the plan of each pass is rebuilt on the device after the
+    // solve (plan_kernel), and kernels past the plan's end exit at once. The host only polls,
+    // without waiting, the active-pair counts that already arrived in pinned memory: to stop
+    // launching once every pair has converged and to shrink the grid of later passes.
+    int64_t total_blk = 0;
+    for (int64_t k = 0; k < npairs; ++k) total_blk += ps[k].nblk;
+    const int64_t per0 = (total_blk + NXCD - 1) / NXCD;
+    int grid = int(std::max<int64_t>(per0 * NXCD, NXCD));
+    int32_t *h_poll = (int32_t *)ctx->host_pinned(size_t(ncnt) * 3 * 4);
+    if (!h_poll) return LSM_ENOMEM;
+    std::vector<hipEvent_t> pass_ev(size_t(ncnt), nullptr);
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
-    int64_t nactive = npairs;
-    std::vector<int32_t> hflags(npairs);
-    int passes = 0;
-    int64_t queries = 0, queries0 = 0;   // source points searched (all passes / first pass)
-    for (int pass = 0; pass <= max_iter && ntasks > 0; ++pass) {
-        hipEvent_t ev;
-        ++passes;
-        if (ctx->timing) {
-            int64_t qn = 0;
-            for (int64_t k = 0; k < npairs; ++k)
-                if (act[k]) qn += ps[k].nsrc;
-            queries += qn;
-            if (pass == 0) queries0 = qn;
+    constexpr int PASS_LAG = 2;
+    plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
+    const TaskPlan tp{d_plan, d_pref, int(npairs)};
+    int passes = 0, polled = 0;
+    int64_t queries = 0, queries0 = 0;   // source points searched (timing mode only)
+    for (int pass = 0; pass <= max_iter; ++pass) {
+        // newest active-pair counts that have landed; waits only to keep at most PASS_LAG
+        // passes queued ahead of the last one read back
+        bool done = false;
+        while (polled < passes) {
+            if (passes - polled > PASS_LAG) {
+                LSM_HIP_TRY(ctx, hipEventSynchronize(pass_ev[size_t(polled)]));
+            } else if (hipEventQuery(pass_ev[size_t(polled)]) != hipSuccess) {
+                break;
+            }
+            const int32_t blocks_left = h_poll[3 * polled + 1];
+            if (h_poll[3 * polled] == 0) done = true;
+            grid = int(std::max<int64_t>(((int64_t(blocks_left) + NXCD - 1) / NXCD) * NXCD, NXCD));
+            ++polled;
         }
+        if (done) break;
+        hipEvent_t ev;
         ctx->tic("nn", &ev);
-        nn_kernel<<<ntasks, NN_THREADS, 0, st>>>(d_tasks, d_ps, d_cd, prm, d_corr, d_cd2, d_q,
-                                                 d_qn + pass, qcap);
+        nn_kernel<<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_cd2, d_q,
+                                               d_qn + pass, qcap);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
         nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass, qcap, d_corr,
@@ -872,65 +947,60 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);
         if (p.method == LSM_P2PLANE)
-            accumulate_kernel<LSM_P2PLANE><<<ntasks, NN_THREADS, 0, st>>>(d_tasks, d_ps, d_cd,
-                                                                          d_corr, d_part);
+            accumulate_kernel<LSM_P2PLANE><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, d_corr,
+                                                                        d_part);
         else
-            accumulate_kernel<LSM_P2P><<<ntasks, NN_THREADS, 0, st>>>(d_tasks, d_ps, d_cd, d_corr,
-                                                                      d_part);
+            accumulate_kernel<LSM_P2P><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, d_corr,
+                                                                    d_part);
         ctx->toc("accumulate", ev);
         ctx->tic("solve", &ev);
         solve_kernel<<<int(npairs), LSM_WAVE, 0, st>>>(d_ps, d_part, prm, pass, d_pbytes,
-                                                       d_active + pass, d_bytes + pass, d_flags);
+                                                       d_active + pass, d_bytes + pass,
+                                                       d_srcn + pass, d_flags);
         ctx->toc("solve", ev);
-        double hb = 0.0;
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(h_active + 2, d_bytes + pass, 8, hipMemcpyDeviceToHost, st));
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(hflags.data(), d_flags, size_t(npairs) * 4,
+        plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass, d_active + pass, 4,
                                         hipMemcpyDeviceToHost, st));
-        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-        std::memcpy(&hb, h_active + 2, 8);
-        int64_t now = 0;
-        for (int64_t k = 0; k < npairs; ++k) now += hflags[k] ? 1 : 0;
-        if (now == 0) break;
-        nn_bytes += hb;
-        if (now != nactive) {      // compact the grid to the pairs still iterating
-            nactive = now;
-            for (int64_t k = 0; k < npairs; ++k) act[k] = hflags[k];
-            tasks = build_tasks(act);
-            ntasks = int(tasks.size());
-            if ((rc = upload(ctx, "i_tasks", tasks, &d_tasks))) return rc;
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass + 1, d_plan, 4, hipMemcpyDeviceToHost,
+                                        st));
+        pass_ev[size_t(pass)] = ctx->get_event();
+        LSM_HIP_TRY(ctx, hipEventRecord(pass_ev[size_t(pass)], st));
+        ++passes;
+    }
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    for (int k = 0; k < passes; ++k) ctx->event_pool.push_back(pass_ev[size_t(k)]);
+    double nn_bytes = 0.0;
+    {
+        std::vector<double> hb(size_t(passes) + 1, 0.0);
+        LSM_HIP_TRY(ctx, hipMemcpy(hb.data(), d_bytes, size_t(passes) * 8, hipMemcpyDeviceToHost));
+        nn_bytes = bytes0;   // pass 0: every pair
+        for (int k = 0; k + 1 < passes; ++k) nn_bytes += hb[size_t(k)];
+        if (ctx->timing) {   // source points searched: all of them, then the active pairs'
+            std::vector<unsigned long long> sn(size_t(passes), 0ull);
+            LSM_HIP_TRY(ctx, hipMemcpy(sn.data(), d_srcn, size_t(passes) * 8,
+                                       hipMemcpyDeviceToHost));
+            queries0 = src_off;
+            queries = src_off;
+            for (int k = 0; k + 1 < passes; ++k) queries += int64_t(sn[size_t(k)]);
         }
     }
     LSM_HIP_TRY(ctx, hipGetLastError());
     // results
     LSM_HIP_TRY(ctx, hipMemcpyAsync(ps.data(), d_ps, ps.size() * sizeof(PairState),
                                     hipMemcpyDeviceToHost, st));
-    // pair 0 correspondences in reference order
+    // pair 0 correspondences in reference order, left on the device until asked for
     {
         const int n0 = int(src[0]->n);
-        int64_t *d_lc = (int64_t *)ctx->buf("i_lastcorr", size_t(std::max(n0, 1)) * 16);
-        uint32_t *d_lcn = (uint32_t *)ctx->buf("i_lastcorr_n", 16);
-        if (!d_lc || !d_lcn) return LSM_ENOMEM;
-        LSM_HIP_TRY(ctx, hipMemsetAsync(d_lcn, 0, 4, st));
+        int32_t *d_dense = (int32_t *)ctx->buf("i_lastcorr_dense", size_t(std::max(n0, 1)) * 4);
+        if (!d_dense) return LSM_ENOMEM;
         if (n0 > 0)
             corr_to_ref<<<(n0 + 255) / 256, 256, 0, st>>>(d_corr, n0, src[0]->d_perm,
-                                                         tgt[0]->d_perm, d_lc, d_lcn);
-        uint32_t m = 0;
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(&m, d_lcn, 4, hipMemcpyDeviceToHost, st));
-        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-        ctx->last_corr.resize(size_t(m) * 2);
-        if (m)
-            LSM_HIP_TRY(ctx, hipMemcpyAsync(ctx->last_corr.data(), d_lc, size_t(m) * 16,
-                                            hipMemcpyDeviceToHost, st));
-        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-        // deterministic order: by source index
-        std::vector<std::pair<int64_t, int64_t>> v(m);
-        for (uint32_t k = 0; k < m; ++k) v[k] = {ctx->last_corr[2 * k], ctx->last_corr[2 * k + 1]};
-        std::sort(v.begin(), v.end());
-        for (uint32_t k = 0; k < m; ++k) {
-            ctx->last_corr[2 * k] = v[k].first;
-            ctx->last_corr[2 * k + 1] = v[k].second;
-        }
+                                                         tgt[0]->d_perm, d_dense);
+        ctx->last_corr_dense_n = n0;
+        ctx->last_corr_pending = true;
+        ctx->last_corr.clear();
     }
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
     ctx->collect_timings();
     if (ctx->timing) {
         ctx->stats["nn"].algo_bytes += nn_bytes;

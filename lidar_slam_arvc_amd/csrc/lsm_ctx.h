@@ -63,8 +63,13 @@ struct lsm_ctx {
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
 
-    // last correspondence set (reference order) of pair 0 of the last ICP call
+    // last correspondence set (reference order) of pair 0 of the last ICP call: the ICP leaves
+    // a dense per-source-point array (target reference index or -1, indexed by the source's
+    // reference index) in the scratch buffer "i_lastcorr_dense"; it is compacted into
+    // last_corr only when asked for (lsm_icp_last_correspondences)
     std::vector<int64_t> last_corr;
+    int64_t last_corr_dense_n = 0;
+    bool last_corr_pending = false;
 
     void set_error(const std::string &e) { err = e; }
     // grow-only named scratch buffer
