@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <unordered_map>
@@ -460,6 +461,29 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
 // ------------------------------------------------------------------------------------------
 // residual / Jacobian accumulation (deterministic block partials)
 // ------------------------------------------------------------------------------------------
+// Wave sums of 32 per-lane values with 32 shuffles instead of 32 x 6: at each butterfly step the
+// lane pair (l, l ^ off) splits the values it still carries, each half keeping one half of the
+// indices summed over both lanes. After the steps with off = 32 .. 2 and a final off = 1 sum,
+// lane l holds the full wave sum of index l >> 1. Fixed tree: deterministic.
+__device__ __forceinline__ double wave_transpose_sum32(double (&v)[32], int lane) {
+#define LSM_TSTEP(OFF, H)                                                     \
+    {                                                                         \
+        const bool up = (lane & (OFF)) != 0;                                  \
+        _Pragma("unroll") for (int k = 0; k < (H); ++k) {                     \
+            const double send = up ? v[k] : v[k + (H)];                       \
+            const double recv = __shfl_xor(send, (OFF), LSM_WAVE);            \
+            v[k] = (up ? v[k + (H)] : v[k]) + recv;                           \
+        }                                                                     \
+    }
+    LSM_TSTEP(32, 16)
+    LSM_TSTEP(16, 8)
+    LSM_TSTEP(8, 4)
+    LSM_TSTEP(4, 2)
+    LSM_TSTEP(2, 1)
+#undef LSM_TSTEP
+    return v[0] + __shfl_xor(v[0], 1, LSM_WAVE);
+}
+
 template <int METHOD>
 __device__ __forceinline__ void accumulate_task(const BlockTask task,
                                                 const PairState *__restrict__ st,
@@ -512,13 +536,13 @@ __device__ __forceinline__ void accumulate_task(const BlockTask task,
             }
         }
     }
-    __shared__ double red[NN_THREADS / LSM_WAVE][30];
+    __shared__ double red[NN_THREADS / LSM_WAVE][32];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double v[32];
 #pragma unroll
-    for (int k = 0; k < 30; ++k) {
-        const double v = lsm_wave_sum(acc[k]);
-        if (lane == 0) red[w][k] = v;
-    }
+    for (int k = 0; k < 32; ++k) v[k] = k < 30 ? acc[k] : 0.0;
+    const double sum = wave_transpose_sum32(v, lane);   // lane l: wave sum of index l >> 1
+    if ((lane & 1) == 0) red[w][lane >> 1] = sum;
     __syncthreads();
     if (threadIdx.x < 30) {
         double s = 0.0;
@@ -915,7 +939,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     if (!h_poll) return LSM_ENOMEM;
     std::vector<hipEvent_t> pass_ev(size_t(ncnt), nullptr);
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
-    constexpr int PASS_LAG = 2;
+    static const int PASS_LAG = [] {   // passes queued ahead of the last one read back
+        const char *e = getenv("LSM_PASS_LAG");
+        return e ? std::max(1, atoi(e)) : 2;
+    }();
     plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
     const TaskPlan tp{d_plan, d_pref, int(npairs)};
     int passes = 0, polled = 0;

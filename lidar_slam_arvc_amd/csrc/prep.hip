@@ -286,35 +286,47 @@ grid_scatter(const Seg *segs, const GridGeo *geo, const CloudDev *cd, const uint
 }
 
 // cell_start[c] = first sorted position with key >= c (lower bound), for c in [0, ncells].
-// One thread per chunk of 32 cells: one binary search, then a merge-walk.
+// One thread per chunk of 32 cells: one binary search, then a merge-walk into LDS; the
+// workgroup's 256 x 32 cells are then stored coalesced (a direct per-thread walk would store
+// 32 consecutive words per lane: 64 cache lines per wave store).
 constexpr int FILL_CHUNK = 32;
+constexpr int FILL_THREADS = 256;
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(FILL_THREADS)
 grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const *cell_out) {
+    __shared__ uint32_t tile[FILL_THREADS * FILL_CHUNK + FILL_THREADS];   // +1 word per row: no conflicts
     const int c = blockIdx.y;
     if (c >= ncloud) return;
     const GridGeo G = geo[c];
-    const int64_t ncells = G.ncells;
-    const int64_t nchunks = (ncells + 1 + FILL_CHUNK - 1) / FILL_CHUNK;
+    const int64_t ncells1 = int64_t(G.ncells) + 1;
     uint32_t *out = cell_out[c];
     const uint64_t *k = skeys + G.pt_off;
-    for (int64_t ch = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; ch < nchunks;
-         ch += int64_t(gridDim.x) * blockDim.x) {
-        const int64_t c0 = ch * FILL_CHUNK;
-        uint32_t lo = 0, hi = G.n;
-        const uint32_t target = G.cell_off + uint32_t(c0);
-        while (lo < hi) {
-            uint32_t mid = (lo + hi) >> 1;
-            if (uint32_t(k[mid] >> 32) < target) lo = mid + 1;
-            else hi = mid;
+    constexpr int64_t PER_WG = int64_t(FILL_THREADS) * FILL_CHUNK;
+    for (int64_t wg0 = int64_t(blockIdx.x) * PER_WG; wg0 < ncells1; wg0 += int64_t(gridDim.x) * PER_WG) {
+        const int64_t c0 = wg0 + int64_t(threadIdx.x) * FILL_CHUNK;
+        uint32_t *row = tile + threadIdx.x * (FILL_CHUNK + 1);
+        if (c0 < ncells1) {
+            uint32_t lo = 0, hi = G.n;
+            const uint32_t target = G.cell_off + uint32_t(c0);
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (uint32_t(k[mid] >> 32) < target) lo = mid + 1;
+                else hi = mid;
+            }
+            uint32_t j = lo;
+#pragma unroll 4
+            for (int i = 0; i < FILL_CHUNK; ++i) {
+                const uint32_t t = target + uint32_t(i);
+                while (j < G.n && uint32_t(k[j] >> 32) < t) ++j;
+                row[i] = j;
+            }
         }
-        uint32_t j = lo;
-        const int64_t c1 = c0 + FILL_CHUNK < ncells + 1 ? c0 + FILL_CHUNK : ncells + 1;
-        for (int64_t cc = c0; cc < c1; ++cc) {
-            const uint32_t t = G.cell_off + uint32_t(cc);
-            while (j < G.n && uint32_t(k[j] >> 32) < t) ++j;
-            out[cc] = j;
+        __syncthreads();
+        for (int e = threadIdx.x; e < int(PER_WG); e += FILL_THREADS) {
+            const int64_t cc = wg0 + e;
+            if (cc < ncells1) out[cc] = tile[(e / FILL_CHUNK) * (FILL_CHUNK + 1) + (e % FILL_CHUNK)];
         }
+        __syncthreads();
     }
 }
 
@@ -1135,9 +1147,9 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         int64_t maxcells = 0;
         for (int k = 0; k < K; ++k)
             maxcells = std::max<int64_t>(maxcells, int64_t(geo[k].ncells) + 1);
-        const int64_t chunks = (maxcells + FILL_CHUNK - 1) / FILL_CHUNK;
-        const int gx = int(std::min<int64_t>((chunks + 255) / 256, 1024));
-        grid_fill<<<dim3(gx, K), 256, 0, st>>>(d_geo, K, k_out, d_cell_ptrs);
+        const int64_t per_wg = int64_t(FILL_THREADS) * FILL_CHUNK;
+        const int gx = int(std::min<int64_t>((maxcells + per_wg - 1) / per_wg, 1024));
+        grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs);
     }
     ctx->toc("grid", ev);
 
