@@ -286,46 +286,83 @@ grid_scatter(const Seg *segs, const GridGeo *geo, const CloudDev *cd, const uint
 }
 
 // cell_start[c] = first sorted position with key >= c (lower bound), for c in [0, ncells].
-// One thread per chunk of 32 cells: one binary search, then a merge-walk into LDS; the
-// workgroup's 256 x 32 cells are then stored coalesced (a direct per-thread walk would store
-// 32 consecutive words per lane: 64 cache lines per wave store).
-constexpr int FILL_CHUNK = 32;
+// One workgroup per tile of FILL_TILE cells: two binary searches bound the tile's points
+// [p0, p1); every cell starts at p1, each cell's first point writes its own position, and a
+// backward min-scan hands empty cells the start of the next occupied one. Keys are read once
+// and the table is written once, coalesced.
 constexpr int FILL_THREADS = 256;
+constexpr int FILL_PER = 16;
+constexpr int FILL_TILE = FILL_THREADS * FILL_PER;
+
+__device__ __forceinline__ uint32_t lower_bound_cell(const uint64_t *k, uint32_t n, uint32_t target) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (uint32_t(k[mid] >> 32) < target) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
 
 __global__ void __launch_bounds__(FILL_THREADS)
 grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const *cell_out) {
-    __shared__ uint32_t tile[FILL_THREADS * FILL_CHUNK + FILL_THREADS];   // +1 word per row: no conflicts
+    __shared__ uint32_t tile[FILL_TILE];
+    __shared__ uint32_t bounds[2];
+    __shared__ uint32_t wmin[FILL_THREADS / LSM_WAVE];
     const int c = blockIdx.y;
     if (c >= ncloud) return;
     const GridGeo G = geo[c];
     const int64_t ncells1 = int64_t(G.ncells) + 1;
     uint32_t *out = cell_out[c];
     const uint64_t *k = skeys + G.pt_off;
-    constexpr int64_t PER_WG = int64_t(FILL_THREADS) * FILL_CHUNK;
-    for (int64_t wg0 = int64_t(blockIdx.x) * PER_WG; wg0 < ncells1; wg0 += int64_t(gridDim.x) * PER_WG) {
-        const int64_t c0 = wg0 + int64_t(threadIdx.x) * FILL_CHUNK;
-        uint32_t *row = tile + threadIdx.x * (FILL_CHUNK + 1);
-        if (c0 < ncells1) {
-            uint32_t lo = 0, hi = G.n;
-            const uint32_t target = G.cell_off + uint32_t(c0);
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (uint32_t(k[mid] >> 32) < target) lo = mid + 1;
-                else hi = mid;
-            }
-            uint32_t j = lo;
-#pragma unroll 4
-            for (int i = 0; i < FILL_CHUNK; ++i) {
-                const uint32_t t = target + uint32_t(i);
-                while (j < G.n && uint32_t(k[j] >> 32) < t) ++j;
-                row[i] = j;
-            }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t c0 = int64_t(blockIdx.x) * FILL_TILE; c0 < ncells1;
+         c0 += int64_t(gridDim.x) * FILL_TILE) {
+        const int64_t c1 = c0 + FILL_TILE < ncells1 ? c0 + FILL_TILE : ncells1;
+        if (threadIdx.x < 2)
+            bounds[threadIdx.x] = lower_bound_cell(k, G.n, G.cell_off + uint32_t(threadIdx.x ? c1 : c0));
+        __syncthreads();
+        const uint32_t p0 = bounds[0], p1 = bounds[1];
+        for (int e = threadIdx.x; e < FILL_TILE; e += FILL_THREADS) tile[e] = p1;
+        __syncthreads();
+        for (uint32_t j = p0 + threadIdx.x; j < p1; j += FILL_THREADS) {
+            const uint32_t cj = uint32_t(k[j] >> 32);
+            if (j == 0 || uint32_t(k[j - 1] >> 32) != cj) tile[cj - G.cell_off - uint32_t(c0)] = j;
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < int(PER_WG); e += FILL_THREADS) {
-            const int64_t cc = wg0 + e;
-            if (cc < ncells1) out[cc] = tile[(e / FILL_CHUNK) * (FILL_CHUNK + 1) + (e % FILL_CHUNK)];
+        // backward min-scan: thread t owns cells [16 t, 16 t + 16)
+        uint32_t v[FILL_PER];
+        uint32_t m = 0xffffffffu;
+#pragma unroll
+        for (int i = FILL_PER - 1; i >= 0; --i) {
+            v[i] = tile[threadIdx.x * FILL_PER + i];
+            m = min(m, v[i]);
         }
+        // minimum over the threads after this one (exclusive suffix), wave then workgroup
+        uint32_t suf = m;
+#pragma unroll
+        for (int off = 1; off < LSM_WAVE; off <<= 1) {
+            const uint32_t o = __shfl_down(suf, off, LSM_WAVE);
+            if (lane + off < LSM_WAVE) suf = min(suf, o);
+        }
+        if (lane == 0) wmin[w] = suf;
+        __syncthreads();
+        uint32_t after = __shfl_down(suf, 1, LSM_WAVE);
+        if (lane == LSM_WAVE - 1) after = 0xffffffffu;
+        for (int q = w + 1; q < FILL_THREADS / LSM_WAVE; ++q) after = min(after, wmin[q]);
+        after = min(after, p1);
+        uint32_t run = after;
+#pragma unroll
+        for (int i = FILL_PER - 1; i >= 0; --i) {
+            run = min(run, v[i]);
+            v[i] = run;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FILL_PER; ++i) tile[threadIdx.x * FILL_PER + i] = v[i];
+        __syncthreads();
+        for (int e = threadIdx.x; e < FILL_TILE; e += FILL_THREADS)
+            if (c0 + e < c1) out[c0 + e] = tile[e];
         __syncthreads();
     }
 }
@@ -1147,8 +1184,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         int64_t maxcells = 0;
         for (int k = 0; k < K; ++k)
             maxcells = std::max<int64_t>(maxcells, int64_t(geo[k].ncells) + 1);
-        const int64_t per_wg = int64_t(FILL_THREADS) * FILL_CHUNK;
-        const int gx = int(std::min<int64_t>((maxcells + per_wg - 1) / per_wg, 1024));
+        const int gx = int(std::min<int64_t>((maxcells + FILL_TILE - 1) / FILL_TILE, 4096));
         grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs);
     }
     ctx->toc("grid", ev);
