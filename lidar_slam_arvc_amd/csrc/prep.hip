@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -397,6 +398,11 @@ __device__ __forceinline__ Off make_off(float4 p, double qx, double qy, double q
     return o;
 }
 
+__device__ __forceinline__ float f32_d2(float4 q, float4 p) {
+    const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+    return dx * dx + dy * dy + dz * dz;
+}
+
 // d^2 < r^2 decided exactly as the f64 reference does: the f32 estimate (relative error
 // < 4e-7 for f32 inputs) settles every point farther than 4e-6 relative from the sphere; the
 // rest take the exact f64 value. The f64 offsets are computed once and shared with the
@@ -520,10 +526,13 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
         }
         a = lo;
     }
+    if (a >= b) return;
+    float4 p = lsm_ld(xyz, a);
     for (uint32_t k = a; k < b; ++k) {
-        const float4 p = lsm_ld(xyz, k);
+        const float4 pn = lsm_ld(xyz, min(k + 1, b - 1));   // next point in flight meanwhile
         if (p.x > xh) break;
         if (p.x >= xl) body(p, k);
+        p = pn;
     }
 }
 
@@ -583,7 +592,8 @@ __device__ __forceinline__ int sel_classify(const Sel &S, double d2, uint32_t k)
 }
 
 __global__ void __launch_bounds__(PT_THREADS)
-normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *stats) {
+normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
+               unsigned long long *stats) {
     __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
     uint32_t *H = lds + threadIdx.x * HSTRIDE;
     uint8_t *H8 = reinterpret_cast<uint8_t *>(H);
@@ -607,15 +617,21 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *s
     Cum c = {};
     ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
-            Off o;
-            if (in_ball(np, qf, qx, qy, qz, p, o)) {
+            auto add = [&](const Off &o) {
                 cum_add(c, o);
                 if (hist) {
                     const int bb = sel_level_bin(S, o.d2, k);
                     const uint32_t v = H8[bb];
-                    if (v == 255u) sat = true;
-                    else H8[bb] = uint8_t(v + 1u);
+                    sat |= v == 255u;
+                    H8[bb] = uint8_t(v + (v < 255u ? 1u : 0u));
                 }
+            };
+            const float f = f32_d2(qf, p);
+            if (f < np.r2_lo) {        // certainly inside: the common case, one branch
+                add(make_off(p, qx, qy, qz));
+            } else if (f <= np.r2_hi) {   // within f32 rounding of the sphere: exact f64 test
+                const Off o = make_off(p, qx, qy, qz);
+                if (o.d2 < np.r2) add(o);
             }
         });
     });
@@ -623,7 +639,7 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *s
         nrm[j] = normal_from_cum(c);
         return;
     }
-    if (stats) atomicAdd(stats, 1u);
+    if (stats) atomicAdd(stats, 1ull);   // points that needed the kNN truncation
     double top = np.r2;   // every point below or member has d2 <= top (up to rounding)
     // rescan the members of the current state: their key extremes and a histogram by `next`
     auto refine = [&](const Sel &next, double &dmin, double &dmax, uint32_t &kmin, uint32_t &kmax) {
@@ -713,8 +729,10 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *s
     uint32_t m = 0;
     ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
-            Off o;
-            if (!in_ball(np, qf, qx, qy, qz, p, o)) return;
+            const float fd = f32_d2(qf, p);
+            if (fd > np.r2_hi) return;
+            const Off o = make_off(p, qx, qy, qz);
+            if (fd >= np.r2_lo && !(o.d2 < np.r2)) return;
             const int cl = sel_classify(S, o.d2, k);
             if (cl < 0) {
                 cum_add(f, o);
@@ -742,6 +760,101 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, uint32_t *s
         if (rank < need) cum_add(f, make_off(lsm_ld(C.xyz, ke), qx, qy, qz));
     }
     nrm[j] = normal_from_cum(f);
+}
+
+// EXPERIMENT (LSM_NORMALS_COOP=1): wave-cooperative scan 1 only (no kNN truncation).
+__device__ __forceinline__ float wave_minf(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, LSM_WAVE));
+    return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, LSM_WAVE));
+    return v;
+}
+__device__ __forceinline__ float bcast(float v, int i) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__global__ void __launch_bounds__(PT_THREADS)
+normals_coop_kernel(const Seg *segs, const CloudDev *cd, NormalParams np) {
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int lane = threadIdx.x & 63;
+    const int j = s.start + threadIdx.x;
+    const int j0 = s.start + (threadIdx.x & ~63);
+    if (j0 >= C.n) return;
+    const bool live = j < C.n;
+    const float4 qf = lsm_ld(C.xyz, live ? j : j0);
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    const float r = np.r;
+    const float prune = r * 1.0001f + 1e-6f, prune2 = prune * prune;
+    const float bx0 = wave_minf(qf.x), bx1 = wave_maxf(qf.x);
+    const float by0 = wave_minf(qf.y), by1 = wave_maxf(qf.y);
+    const float bz0 = wave_minf(qf.z), bz1 = wave_maxf(qf.z);
+    auto rng = [&](float lo, float hi, float o, int n, int &a, int &b) {
+        a = max((int)floorf((lo - r - o) * C.inv_cell - 1e-3f), 0);
+        b = min((int)floorf((hi + r - o) * C.inv_cell + 1e-3f), n - 1);
+    };
+    int xlo, xhi, ylo, yhi, zlo, zhi;
+    rng(bx0, bx1, C.ox, C.nx, xlo, xhi);
+    rng(by0, by1, C.oy, C.ny, ylo, yhi);
+    rng(bz0, bz1, C.oz, C.nz, zlo, zhi);
+    Cum c = {};
+    const float *xs = reinterpret_cast<const float *>(C.xyz);
+    for (int z = zlo; z <= zhi; ++z) {
+        const float dz2 = slab_d2(qf.z, C.oz, C.cell, z);
+        for (int y = ylo; y <= yhi; ++y) {
+            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
+            const bool act = live && dyz2 <= prune2;
+            if (!__ballot(act)) continue;
+            const float ch = act ? sqrtf(prune2 - dyz2) * 1.0001f + 1e-6f * fabsf(qf.x) + 1e-5f : 0.f;
+            const float xl = wave_minf(act ? qf.x - ch : INFINITY);
+            const float xh = wave_maxf(act ? qf.x + ch : -INFINITY);
+            const int xa = max(xlo, (int)floorf((xl - C.ox) * C.inv_cell - 1e-3f));
+            const int xb = min(xhi, (int)floorf((xh - C.ox) * C.inv_cell + 1e-3f));
+            int x = xa;
+            while (x <= xb) {
+                const int xe = min(xb, x | (LSM_BLK - 1));
+                const uint32_t a = uni(lsm_ld(C.cell_start, lsm_cell_lin(C.nbx, C.nby, x, y, z)));
+                const uint32_t b = uni(lsm_ld(C.cell_start, lsm_cell_lin(C.nbx, C.nby, xe, y, z) + 1));
+                x = xe + 1;
+                if (b <= a) continue;
+                uint32_t lo = a, hi = b;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (lsm_ld(xs, size_t(mid) * 4) < xl) lo = mid + 1;
+                    else hi = mid;
+                }
+                lo = uni(lo);
+                bool stop = false;
+                for (uint32_t base = lo; base < b && !stop; base += LSM_WAVE) {
+                    const uint32_t idx = min(base + lane, b - 1);
+                    const float4 p = lsm_ld(C.xyz, idx);
+                    const int cnt = int(min(b - base, uint32_t(LSM_WAVE)));
+                    for (int i = 0; i < cnt; ++i) {
+                        const float px = bcast(p.x, i);
+                        if (px > xh) {
+                            stop = true;
+                            break;
+                        }
+                        const float py = bcast(p.y, i), pz = bcast(p.z, i);
+                        const float dx = qf.x - px, dy = qf.y - py, dz = qf.z - pz;
+                        const float f = dx * dx + dy * dy + dz * dz;
+                        const bool maybe = act && f <= np.r2_hi;
+                        if (!__ballot(maybe)) continue;
+                        if (maybe) {
+                            const Off o = make_off(make_float4(px, py, pz, 0.f), qx, qy, qz);
+                            if (f < np.r2_lo || o.d2 < np.r2) cum_add(c, o);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (live) const_cast<float4 *>(C.nrm)[j] = normal_from_cum(c);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1198,7 +1311,25 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         np.r2_hi = float(np.r2 * (1.0 + 4e-6));
         np.max_nn = p.max_nn;
         ctx->tic("normals", &ev);
-        normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, nullptr);
+        static const bool coop = getenv("LSM_NORMALS_COOP") != nullptr;
+        if (coop)
+            normals_coop_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np);
+        else
+        {
+            static const bool nstats = getenv("LSM_NORMALS_STATS") != nullptr;
+            unsigned long long *d_ns = nullptr;
+            if (nstats) {
+                d_ns = (unsigned long long *)ctx->buf("n_stats", 8 * 8);
+                LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 64, st));
+            }
+            normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
+            if (nstats) {
+                unsigned long long h = 0;
+                LSM_HIP_TRY(ctx, hipMemcpyAsync(&h, d_ns, 8, hipMemcpyDeviceToHost, st));
+                LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+                ctx->stats["normals_truncated"].launches += int64_t(h);
+            }
+        }
         ctx->toc("normals", ev);
     }
 

@@ -20,3 +20,12 @@ for r, mnn in CASES:
     dev.set_timing(False)
     st = {k: dev.kernel_stats(k)["ms"] / 5 for k in ("grid", "normals")}
     print(f"r={r} max_nn={mnn}: " + " ".join(f"{k}={v:.3f}ms" for k, v in st.items()), flush=True)
+if os.environ.get("LSM_NORMALS_STATS"):
+    dev.reset_stats()
+    dev.preprocess(ids, _lib.prep_params())
+    names = ["ns_points", "ns_scan1_iters", "ns_selecting", "ns_refines", "ns_refine_iters",
+             "ns_final_iters", "ns_box"]
+    v = {k: dev.kernel_stats(k)["launches"] for k in names}
+    n = v["ns_points"]
+    print({k: round(x / n, 3) for k, x in v.items()}, "per point; selecting:",
+          v["ns_selecting"], "final iters per selecting", v["ns_final_iters"] / max(v["ns_selecting"], 1))
