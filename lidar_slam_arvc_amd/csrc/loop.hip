@@ -20,18 +20,18 @@
 namespace {
 
 __device__ __forceinline__ double norm_dot(double x, double y, double z) {
-    return sqrt(__fma_rn(z, z, __fma_rn(y, y, __dmul_rn(x, x))));
+    return sqrt(fma(z, z, fma(y, y, lsm_dmul(x, x))));
 }
 
 __device__ __forceinline__ double norm_rows(double x, double y, double z) {
-    return sqrt(__dadd_rn(__dadd_rn(__dmul_rn(x, x), __dmul_rn(y, y)), __dmul_rn(z, z)));
+    return sqrt(lsm_dadd(lsm_dadd(lsm_dmul(x, x), lsm_dmul(y, y)), lsm_dmul(z, z)));
 }
 
 __global__ void segment_lengths(const double *P, int64_t m, double *seg) {
     const int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (k + 1 >= m) return;
-    seg[k] = norm_dot(__dsub_rn(P[3 * (k + 1)], P[3 * k]), __dsub_rn(P[3 * (k + 1) + 1], P[3 * k + 1]),
-                      __dsub_rn(P[3 * (k + 1) + 2], P[3 * k + 2]));
+    seg[k] = norm_dot(lsm_dsub(P[3 * (k + 1)], P[3 * k]), lsm_dsub(P[3 * (k + 1) + 1], P[3 * k + 1]),
+                      lsm_dsub(P[3 * (k + 1) + 2], P[3 * k + 2]));
 }
 
 __global__ void walk_back(const double *seg, int64_t m, double dback, int64_t *index) {
@@ -39,7 +39,7 @@ __global__ void walk_back(const double *seg, int64_t m, double dback, int64_t *i
     double d = 0.0;
     int64_t out = -1;
     for (int64_t i = m - 2; i >= 0; --i) {
-        d = __dadd_rn(d, seg[i]);
+        d = lsm_dadd(d, seg[i]);
         if (d > dback) {
             out = i;
             break;
@@ -67,8 +67,8 @@ within_radius(const double *P, int64_t m, const int64_t *index, double radius, i
         const int64_t k = s + threadIdx.x;
         bool keep = false;
         if (k < idx) {
-            const double d = norm_rows(__dsub_rn(P[3 * k], cx), __dsub_rn(P[3 * k + 1], cy),
-                                       __dsub_rn(P[3 * k + 2], cz));
+            const double d = norm_rows(lsm_dsub(P[3 * k], cx), lsm_dsub(P[3 * k + 1], cy),
+                                       lsm_dsub(P[3 * k + 2], cz));
             keep = d < radius;
         }
         const uint64_t mk = __ballot(keep);
@@ -97,8 +97,8 @@ __global__ void partners_kernel(const double *P, const int64_t *cand, int64_t n,
         const int64_t u = cand[q];
         const int64_t di = u > j1 ? u - j1 : j1 - u;
         if (!(di > 1 && di < 80)) continue;
-        const double de = norm_dot(__dsub_rn(P[3 * j1], P[3 * u]), __dsub_rn(P[3 * j1 + 1], P[3 * u + 1]),
-                                   __dsub_rn(P[3 * j1 + 2], P[3 * u + 2]));
+        const double de = norm_dot(lsm_dsub(P[3 * j1], P[3 * u]), lsm_dsub(P[3 * j1 + 1], P[3 * u + 1]),
+                                   lsm_dsub(P[3 * j1 + 2], P[3 * u + 2]));
         if (de > 1.0 && de < 2.0) {
             out = u;
             break;

@@ -78,12 +78,33 @@ struct BlockTask {
         }                                                                               \
     } while (0)
 
+// Correctly rounded f64 operations that the compiler may NOT fuse into an FMA (hipcc contracts
+// a * b + c by default, and HIP's __dmul_rn / __dadd_rn are plain operators): the bit-exact
+// paths (filter mask, distances that decide neighbourhood membership, loop-closure norms)
+// must round every product and sum separately, as NumPy / nanoflann do.
+__device__ __forceinline__ double lsm_dmul(double a, double b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
+__device__ __forceinline__ double lsm_dadd(double a, double b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+__device__ __forceinline__ double lsm_dsub(double a, double b) {
+#pragma clang fp contract(off)
+    return a - b;
+}
+__device__ __forceinline__ double lsm_ddiv(double a, double b) {
+#pragma clang fp contract(off)
+    return a / b;
+}
+
 // Exact nanoflann-style squared distance in f64 without contraction:
 // ((dx*dx + dy*dy) + dz*dz), dx = q - p (L2_Adaptor::evalMetric order).
 __device__ __forceinline__ double lsm_sqdist64(double qx, double qy, double qz, double px,
                                                double py, double pz) {
-    double dx = __dsub_rn(qx, px), dy = __dsub_rn(qy, py), dz = __dsub_rn(qz, pz);
-    return __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+    double dx = lsm_dsub(qx, px), dy = lsm_dsub(qy, py), dz = lsm_dsub(qz, pz);
+    return lsm_dadd(lsm_dadd(lsm_dmul(dx, dx), lsm_dmul(dy, dy)), lsm_dmul(dz, dz));
 }
 
 // Loads through a global-address-space view of a device pointer that was read from a

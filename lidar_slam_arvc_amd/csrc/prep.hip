@@ -47,7 +47,7 @@ struct FilterParams {
 
 __device__ __forceinline__ bool keep_point(float x, float y, float z, const FilterParams &f) {
     double dx = x, dy = y, dz = z;
-    double r2 = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+    double r2 = lsm_dadd(lsm_dmul(dx, dx), lsm_dmul(dy, dy));
     return (r2 < f.maxr2) & (r2 > f.minr2) & (dz > f.minh) & (dz < f.maxh);
 }
 
@@ -170,9 +170,9 @@ voxel_keys(const Seg *segs, const float4 *pts, const uint32_t *cloud_off, const 
     const VoxGeo G = geo[s.cloud];
     float4 p = pts[g];
     // ref_coord = (p - voxel_min_bound) / voxel_size ; voxel_index = int(floor(ref_coord))
-    int64_t kx = (int64_t)(int)floor(__ddiv_rn(__dsub_rn((double)p.x, G.ox), v));
-    int64_t ky = (int64_t)(int)floor(__ddiv_rn(__dsub_rn((double)p.y, G.oy), v));
-    int64_t kz = (int64_t)(int)floor(__ddiv_rn(__dsub_rn((double)p.z, G.oz), v));
+    int64_t kx = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.x, G.ox), v));
+    int64_t ky = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.y, G.oy), v));
+    int64_t kz = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.z, G.oz), v));
     keys[g] = G.key_off + uint64_t((kx * G.dy + ky) * G.dz + kz);
     vals[g] = g;
 }
@@ -197,13 +197,13 @@ voxel_reduce(const uint64_t *skeys, const uint32_t *svals, const uint32_t *vid_e
     uint32_t j = i;
     for (; j < n && skeys[j] == key; ++j) {
         float4 p = pts[svals[j]];
-        sx = __dadd_rn(sx, (double)p.x);
-        sy = __dadd_rn(sy, (double)p.y);
-        sz = __dadd_rn(sz, (double)p.z);
+        sx = lsm_dadd(sx, (double)p.x);
+        sy = lsm_dadd(sy, (double)p.y);
+        sz = lsm_dadd(sz, (double)p.z);
     }
     const double cnt = double(j - i);
     const uint32_t o = vid_excl[i];
-    const double cx = __ddiv_rn(sx, cnt), cy = __ddiv_rn(sy, cnt), cz = __ddiv_rn(sz, cnt);
+    const double cx = lsm_ddiv(sx, cnt), cy = lsm_ddiv(sy, cnt), cz = lsm_ddiv(sz, cnt);
     cent[3 * o] = cx;
     cent[3 * o + 1] = cy;
     cent[3 * o + 2] = cz;
@@ -388,13 +388,13 @@ struct Off {
 
 __device__ __forceinline__ Off make_off(float4 p, double qx, double qy, double qz) {
     Off o;
-    o.dx = __dsub_rn((double)p.x, qx);
-    o.dy = __dsub_rn((double)p.y, qy);
-    o.dz = __dsub_rn((double)p.z, qz);
-    o.xx = __dmul_rn(o.dx, o.dx);
-    o.yy = __dmul_rn(o.dy, o.dy);
-    o.zz = __dmul_rn(o.dz, o.dz);
-    o.d2 = __dadd_rn(__dadd_rn(o.xx, o.yy), o.zz);
+    o.dx = lsm_dsub((double)p.x, qx);
+    o.dy = lsm_dsub((double)p.y, qy);
+    o.dz = lsm_dsub((double)p.z, qz);
+    o.xx = lsm_dmul(o.dx, o.dx);
+    o.yy = lsm_dmul(o.dy, o.dy);
+    o.zz = lsm_dmul(o.dz, o.dz);
+    o.d2 = lsm_dadd(lsm_dadd(o.xx, o.yy), o.zz);
     return o;
 }
 
@@ -605,9 +605,7 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     const double qx = qf.x, qy = qf.y, qz = qf.z;
     float4 *nrm = const_cast<float4 *>(C.nrm);
     // candidates in the ball's cells: when they cannot exceed max_nn, no selection is needed
-    uint32_t box = 0;
-    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float, float) { box += b - a; });
-    const bool hist = box > uint32_t(np.max_nn);
+    const bool hist = true;
     if (hist) {
 #pragma unroll
         for (int b = 0; b < NB8 / 4; ++b) H[b] = 0;
