@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs-per-gpu", type=int, default=64)
+    ap.add_argument("--pairs-per-gpu", type=int, default=256)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
     ap.add_argument("--cpu-sample-pairs", type=int, default=2)
@@ -121,7 +121,7 @@ def main():
         dt = float(t.item())
 
     stats = {k: dev.kernel_stats(k) for k in KERNELS}
-    nn = stats["nn"]
+    nn = dev.kernel_stats("nn_pass")   # check + search + fallback of every ICP pass
     n_pts, res = last
     iters = [r["iterations"] for r in res]
     out = None
@@ -134,10 +134,13 @@ def main():
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "kernel": "nn_kernel",
+                "kernel": "correspondence pass: nn_kernel (stability check + box search) + "
+                          "nn_fallback",
                 "algo_bytes_per_launch": nn["algo_bytes"] / max(nn["launches"], 1),
                 "avg_launch_ms": nn["ms"] / max(nn["launches"], 1),
-                "launches": nn["launches"]}
+                "launches": nn["launches"],
+                "per_kernel_ms_per_pass": {k: round(stats[k]["ms"] / max(nn["launches"], 1), 5)
+                                           for k in ("nn", "nn_fallback")}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(seq, args.cpu_sample_pairs, args.method, args.cpu_threads)
@@ -167,7 +170,11 @@ def main():
             "mean_icp_iterations": float(np.mean(iters)),
             "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
                                       for k, v in stats.items() if v["launches"]},
-            "nn_fallback_fraction": {
+            "nn_uncertified_fraction_after_pass0": round(
+            dev.kernel_stats("nn_uncertified")["launches"] /
+            max(dev.kernel_stats("nn_queries")["launches"] -
+                dev.kernel_stats("nn_queries_first_pass")["launches"], 1), 5),
+        "nn_fallback_fraction": {
                 "all_passes": round(dev.kernel_stats("nn_pending")["launches"] /
                                     max(dev.kernel_stats("nn_queries")["launches"], 1), 5),
                 "first_pass": round(dev.kernel_stats("nn_pending_first_pass")["launches"] /

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -43,11 +44,21 @@ struct NNParams {
     double rel_fit, rel_rmse;
 };
 
+// Correspondence state of one source point, carried from pass to pass (SoA arrays):
+//   corr[i]  nearest target point (sorted index), -1 = none within max_corr
+//   rho[i]   a lower bound on the distance from the pass's f32 query point q_i to every target
+//            point OTHER than corr[i] (to every point when corr[i] = -1), metres.
+// Stability certificate: if q_i moves by delta between passes and |q_i - t_corr| + delta < rho,
+// no other point can have come nearer than t_corr, so the nearest neighbour is unchanged and
+// needs no search (rho <- rho - delta). Later ICP passes move the source by micrometres to
+// millimetres, so nearly every query of a converging pair is certified with two loads.
 struct FallbackItem {
     int32_t pair;
     int32_t i;        // source point (sorted order)
-    int32_t best;     // best target index found by nn_kernel (-1 none)
+    int32_t best;     // best target index found by the box search (-1 none)
     float best_d2;
+    float second_d2;  // second-smallest distance examined (a point other than best)
+    float margin;     // rho margin of this query (see prune2)
 };
 
 __device__ __forceinline__ bool better(float d2, int idx, float bd2, int bidx) {
@@ -62,26 +73,60 @@ __device__ __forceinline__ void transform_point(const double *T, float4 p, doubl
     z = T[8] * px + T[9] * py + T[10] * pz + T[11];
 }
 
-__device__ __forceinline__ void try_point(const float4 t, uint32_t k, float qx, float qy, float qz,
-                                          float &bd2, int &bidx) {
-    const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
-    const float d2 = dx * dx + dy * dy + dz * dz;
-    if (better(d2, int(k), bd2, bidx)) {
-        bd2 = d2;
-        bidx = int(k);
+// Running (nearest, second-nearest) over examined target points. A point is examined at most
+// once as the current best (k == bidx is skipped: the warm-start point is revisited by the box
+// scan), so the second distance always belongs to a different point.
+// `lim` caches prune2(): the squared pruning radius, refreshed whenever bd2 or sd2 changes.
+struct Top2 {
+    float bd2;
+    int bidx;
+    float sd2;
+    float lim;
+    float m;   // margin of prune2
+};
+
+// Squared pruning radius of a search: the second-best distance, capped at (best + m)^2 and
+// never below the best (ties with the best are always examined, so the (d2, index) minimum is
+// exact). Every point the search skips is at least this far, so it is a valid rho (the radius
+// only shrinks during a search). m = 0 gives a plain nearest-neighbour search (rho = best
+// distance: certifies nothing); m = 4 x (this pass's displacement) + 1 mm leaves room for the
+// next passes' motion.
+__device__ __forceinline__ float prune2(float bd2, float sd2, float m) {
+    const float c = __builtin_amdgcn_sqrtf(bd2) + m;
+    return fmaxf(bd2, fminf(sd2, c * c));
+}
+
+__device__ __forceinline__ Top2 top2_init(int bidx, float bd2, float sd2, float m) {
+    return Top2{bd2, bidx, sd2, prune2(bd2, sd2, m), m};
+}
+
+__device__ __forceinline__ void top2_add(float d2, int k, Top2 &b) {
+    if (k == b.bidx || !(d2 < b.sd2 || (d2 == b.bd2 && k < b.bidx))) return;
+    if (better(d2, k, b.bd2, b.bidx)) {
+        b.sd2 = b.bd2;
+        b.bd2 = d2;
+        b.bidx = k;
+    } else {
+        b.sd2 = d2;
     }
+    b.lim = prune2(b.bd2, b.sd2, b.m);
+}
+
+__device__ __forceinline__ float sqd(const float4 t, float qx, float qy, float qz) {
+    const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
+    return dx * dx + dy * dy + dz * dz;
 }
 
 // One x-sorted run [a, b) of a cell row whose slab is at least dyz2 (squared, underestimated)
 // from the query: enter at the query's x (binary search on long runs) and walk outwards while
-// dx^2 + dyz2 <= best (strict '>' stops: equal distances are still examined, so (d2, index)
-// ties resolve exactly as a full scan would).
+// dx^2 + dyz2 <= the pruning radius (strict '>' stops: equal distances are still examined, so
+// (d2, index) ties resolve exactly as a full scan would).
 constexpr uint32_t NN_LINEAR = 8;
 
 __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float qx,
-                                         float qy, float qz, float dyz2, float &bd2, int &bidx) {
+                                         float qy, float qz, float dyz2, Top2 &t2) {
     if (b - a <= NN_LINEAR) {
-        for (uint32_t k = a; k < b; ++k) try_point(lsm_ld(xyz, k), k, qx, qy, qz, bd2, bidx);
+        for (uint32_t k = a; k < b; ++k) top2_add(sqd(lsm_ld(xyz, k), qx, qy, qz), int(k), t2);
         return;
     }
     const float *xs = reinterpret_cast<const float *>(xyz);
@@ -94,16 +139,23 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
     for (uint32_t k = lo; k < b; ++k) {
         const float4 t = lsm_ld(xyz, k);
         const float dx = t.x - qx;
-        if (dx * dx + dyz2 > bd2) break;
-        try_point(t, k, qx, qy, qz, bd2, bidx);
+        if (dx * dx + dyz2 > t2.lim) break;
+        top2_add(sqd(t, qx, qy, qz), int(k), t2);
     }
     for (uint32_t k = lo; k > a;) {
         --k;
         const float4 t = lsm_ld(xyz, k);
         const float dx = qx - t.x;
-        if (dx * dx + dyz2 > bd2) break;
-        try_point(t, k, qx, qy, qz, bd2, bidx);
+        if (dx * dx + dyz2 > t2.lim) break;
+        top2_add(sqd(t, qx, qy, qz), int(k), t2);
     }
+}
+
+// Conservative lower-bound radius from a squared f32 distance / an f32 box bound (metres):
+// covers the f32 rounding of distances and of the grid's cell coordinates.
+__device__ __forceinline__ float rho_from(float d2, float bound) {
+    const float r = fminf(sqrtf(d2), bound);
+    return r == INFINITY ? INFINITY : fmaxf(r * (1.f - 1e-5f) - 2e-5f, 0.f);
 }
 
 // squared distance (in cells^2) from fractional coordinate f to cell k's slab [k, k+1)
@@ -186,152 +238,254 @@ __device__ __forceinline__ int plan_task(const TaskPlan &tp, const PairState *st
 // ------------------------------------------------------------------------------------------
 // correspondence search (the hot kernel)
 // ------------------------------------------------------------------------------------------
-// Search box: the cells within the warm-start radius R = sqrt(previous neighbour's distance)
-// (at most NN_KMAX cells each way), or the 3x3x3 block around the query's cell on a cold start.
-// Rows of cells are visited centre-out and pruned by their slab distance; inside a row the
-// x-sorted runs are walked from the query's x. A query is resolved when its best distance is
-// provably below every unsearched point (the box faces not clipped by the grid), else queued.
+// One workgroup per block of 256 source points of an active pair (XCD-balanced work plan).
+// Passes >= 1 first run the stability check on every point (two loads per query: the source
+// point and its previous neighbour); the queries it cannot certify are compacted in LDS and
+// box-searched by the leading lanes, so whole waves of certified queries retire at once. Pass 0
+// (and every pass with LSM_NN_NOCERT=1) box-searches every point. Queries the box search cannot
+// resolve go to nn_fallback. Every path computes the same (d2, index) minimum with the same f32
+// arithmetic, so the result does not depend on which path resolved a query.
+//
+// Box search: the cells within the warm-start radius R = sqrt(previous neighbour's distance)
+// (at most NN_KMAX cells each way), or the 5x5x5 cells around the query's cell on a cold start.
+// Rows of cells are visited centre-out and pruned by their slab distance against the pruning
+// radius (prune2: it yields rho); inside a row the x-sorted runs are walked from the query's x.
+// A query is resolved when its best distance is provably below every unsearched point (the box
+// faces not clipped by the grid), else queued for the fallback.
 constexpr int NN_KMAX = 4;
 constexpr int NN_KCOLD = 2;   // cold start (no previous neighbour): 5x5x5 cells
 
-__device__ __forceinline__ void nn_task(const BlockTask task, const PairState *__restrict__ st,
-                                        const CloudDev *__restrict__ cds, const NNParams &prm,
-                                        int32_t *__restrict__ corr, float *__restrict__ corr_d2,
-                                        FallbackItem *__restrict__ queue,
-                                        uint32_t *__restrict__ queue_n, uint32_t queue_cap) {
+// Returns true when resolved (result / rho set), false when the fallback must finish it (t2
+// holds what the box search found).
+__device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, const CloudDev &G,
+                                         int i, int prev, float m, const NNParams &prm,
+                                         int &result, float &rho, Top2 &t2) {
+    double qx64, qy64, qz64;
+    transform_point(T, lsm_ld(S.xyz, i), qx64, qy64, qz64);
+    const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
+    t2 = top2_init(-1, INFINITY, INFINITY, m);
+    result = -1;
+    rho = INFINITY;
+    if (G.n <= 0) return true;
+    // warm start: the previous pass's nearest neighbour bounds this pass's search. The search
+    // stays exact -- the (d2, index) minimum over all points does not depend on the start.
+    if (prev >= 0 && prev < G.n) t2 = top2_init(prev, sqd(lsm_ld(G.xyz, prev), qx, qy, qz), INFINITY, m);
+    const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
+                fz = (qz - G.oz) * G.inv_cell;
+    // a query outside the target's box searches around the nearest cell of the box: the
+    // box faces that lie on the grid boundary bound nothing (no points beyond them)
+    auto clampc = [](float f, int n) { return (int)fminf(fmaxf(floorf(f), 0.f), float(n - 1)); };
+    const int cx = clampc(fx, G.nx), cy = clampc(fy, G.ny), cz = clampc(fz, G.nz);
+    // box half-width in cells: the warm-start radius (+ f32 slack), else NN_KCOLD
+    int K = NN_KCOLD;
+    if (t2.bd2 < INFINITY) {
+        const float rc = sqrtf(t2.bd2) * G.inv_cell * 1.0001f + 1e-4f;
+        K = rc >= float(NN_KMAX) ? NN_KMAX : max(1, (int)ceilf(rc));
+    }
+    const int x0 = max(cx - K, 0), x1 = min(cx + K, G.nx - 1);
+    const int y0 = max(cy - K, 0), y1 = min(cy + K, G.ny - 1);
+    const int z0 = max(cz - K, 0), z1 = min(cz + K, G.nz - 1);
+    const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
+    const uint32_t *cs = G.cell_start;
+#pragma unroll 1
+    for (int iz = 0; iz <= 2 * K; ++iz) {
+        const int dz = (iz & 1) ? -((iz + 1) >> 1) : (iz >> 1);   // 0, -1, 1, -2, 2 ...
+        const int z = cz + dz;
+        if (z < z0 || z > z1) continue;
+        const float wz = slab_cells2(fz, z) * c2;
+        if (wz >= t2.lim) continue;
+#pragma unroll 1
+        for (int iy = 0; iy <= 2 * K; ++iy) {
+            const int dy = (iy & 1) ? -((iy + 1) >> 1) : (iy >> 1);
+            const int y = cy + dy;
+            if (y < y0 || y > y1) continue;
+            const float wyz = wz + slab_cells2(fy, y) * c2;
+            const float lim = t2.lim;
+            if (wyz >= lim) continue;
+            // cells of this row that can still hold a point within the pruning radius
+            int xa = x0, xb = x1;
+            if (lim < INFINITY) {
+                const float ch = sqrtf((lim - wyz) * 1.0002f) * G.inv_cell + 1e-4f;
+                xa = max(xa, (int)floorf(fx - ch));
+                xb = min(xb, (int)floorf(fx + ch));
+            }
+            int x = xa;
+            while (x <= xb) {
+                const int xe = min(xb, x | (LSM_BLK - 1));   // end of this block's row part
+                const uint32_t a = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, x, y, z));
+                const uint32_t b = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, xe, y, z) + 1);
+                if (b > a) scan_run(G.xyz, a, b, qx, qy, qz, wyz, t2);
+                x = xe + 1;
+            }
+        }
+    }
+    // every point outside the searched box is at least `bound` away; sides clipped by the grid
+    // hold no points.
+    const float bx = fminf(cx - K > 0 ? fx - float(cx - K) : INFINITY,
+                           cx + K + 1 < G.nx ? float(cx + K + 1) - fx : INFINITY);
+    const float by = fminf(cy - K > 0 ? fy - float(cy - K) : INFINITY,
+                           cy + K + 1 < G.ny ? float(cy + K + 1) - fy : INFINITY);
+    const float bz = fminf(cz - K > 0 ? fz - float(cz - K) : INFINITY,
+                           cz + K + 1 < G.nz ? float(cz + K + 1) - fz : INFINITY);
+    const float bound = fminf(bx, fminf(by, bz)) * G.cell;
+    const float bound2 = bound * bound * 0.99999f;
+    if (t2.bd2 <= bound2 || bound >= prm.maxc) {
+        if (t2.bidx >= 0 && t2.bd2 < prm.maxc2) {
+            result = t2.bidx;
+            rho = rho_from(t2.lim, bound);
+        } else {
+            result = -1;
+            rho = rho_from(t2.bd2, bound);
+        }
+        return true;
+    }
+    return false;
+}
+
+// wave-aggregated append of the lanes with `pending` to the fallback queue
+__device__ __forceinline__ void push_fallback(bool pending, int pair, int i, float m,
+                                              const Top2 &t2,
+                                              FallbackItem *__restrict__ queue,
+                                              uint32_t *__restrict__ queue_n, uint32_t queue_cap) {
+    const uint64_t bm = __ballot(pending);
+    if (!bm) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)bm) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(queue_n, (uint32_t)__popcll(bm));
+    base = __shfl(base, leader, LSM_WAVE);
+    if (pending) {
+        const uint32_t slot = base + __popcll(bm & ((uint64_t(1) << lane) - 1));
+        if (slot < queue_cap) queue[slot] = {pair, i, t2.bidx, t2.bd2, t2.sd2, m};
+    }
+}
+
+// Stability check of one query (passes >= 1). delta = |q - q'| between this pass's and the
+// previous pass's f32 query points (both recomputed from the stored transforms, f64 difference
+// of f32 values). Certified: |q - t_corr| (1 + 1e-5) + delta < rho, i.e. every other point is
+// strictly farther even after the f32 rounding of the search's squared distances (relative
+// error < 1e-6); the neighbour stays (or drops out when it left max_corr) and rho shrinks by
+// delta, rounded down. A query without a neighbour stays without one while
+// rho - delta >= max_corr (1 + 1e-5). Returns false when the query must be searched; `m` is
+// then its margin for the search's rho.
+__device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &S,
+                                           const CloudDev &G, int i, int64_t g,
+                                           const NNParams &prm, int32_t *__restrict__ corr,
+                                           float *__restrict__ rho, float &m) {
+    const float4 s = lsm_ld(S.xyz, i);
+    double x, y, z, xp, yp, zp;
+    transform_point(P.T, s, x, y, z);
+    transform_point(P.Tp, s, xp, yp, zp);
+    const float qx = float(x), qy = float(y), qz = float(z);
+    const double ddx = double(qx) - double(float(xp)), ddy = double(qy) - double(float(yp)),
+                 ddz = double(qz) - double(float(zp));
+    const double dq = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
+    const double delta = dq * (1.0 + 1e-6) + 1e-7;
+    m = float(4.0 * dq + 1e-3);
+    const int prev = corr[g];
+    const double r = double(rho[g]);
+    if (prev >= 0) {
+        const float4 t = lsm_ld(G.xyz, prev);
+        const double ex = double(qx) - double(t.x), ey = double(qy) - double(t.y),
+                     ez = double(qz) - double(t.z);
+        const double e = sqrt(ex * ex + ey * ey + ez * ez);
+        if (!(e * (1.0 + 1e-5) + delta < r)) return false;
+        if (sqd(t, qx, qy, qz) < prm.maxc2) {
+            rho[g] = __double2float_rd(r - delta);
+        } else {   // the neighbour left max_corr: no point is within it, none nearer than e
+            corr[g] = -1;
+            rho[g] = __double2float_rd(fmin(e * (1.0 - 1e-5), r - delta));
+        }
+        return true;
+    }
+    if (prev == -1 && r - delta >= double(prm.maxc) * (1.0 + 1e-5)) {
+        rho[g] = __double2float_rd(r - delta);
+        return true;
+    }
+    return false;
+}
+
+template <bool CHECK>
+__global__ void __launch_bounds__(NN_THREADS)
+nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
+          NNParams prm, int32_t *__restrict__ corr, float *__restrict__ rho,
+          FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n, uint32_t queue_cap,
+          uint32_t *__restrict__ searched) {
+    // one task per workgroup: the host sizes the grid from an earlier pass's plan, which only
+    // shrinks, so waves may retire early (no barrier follows the compaction)
+    BlockTask task;
+    if (plan_task(tp, st, blockIdx.x, task) <= 0) return;
     const PairState &P = st[task.pair];
     if (!P.active) return;
     const CloudDev S = cds[P.src];
     const CloudDev G = cds[P.tgt];
-    const int i = task.start + threadIdx.x;
-    const bool live = i < S.n;
+    int i = task.start + threadIdx.x;
+    bool live = i < S.n;
+    float m = 0.f;
+    if (CHECK) {
+        __shared__ int32_t s_idx[NN_THREADS];
+        __shared__ float s_m[NN_THREADS];
+        __shared__ int32_t s_cnt[NN_THREADS / LSM_WAVE];
+        bool need = false;
+        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, rho, m);
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const uint64_t bm = __ballot(need);
+        if (lane == 0) s_cnt[w] = __popcll(bm);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int q = 0; q < NN_THREADS / LSM_WAVE; ++q) {
+            before += q < w ? s_cnt[q] : 0;
+            total += s_cnt[q];
+        }
+        if (need) {
+            const int slot = before + __popcll(bm & ((uint64_t(1) << lane) - 1));
+            s_idx[slot] = i;
+            s_m[slot] = m;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && total > 0) atomicAdd(searched, uint32_t(total));
+        if (w * LSM_WAVE >= total) return;   // this wave has nothing to search
+        live = int(threadIdx.x) < total;
+        if (live) {
+            i = s_idx[threadIdx.x];
+            m = s_m[threadIdx.x];
+        }
+    }
+    const int64_t g = P.src_off + i;
     int result = -1;
-    float bd2 = INFINITY;
-    int bidx = -1;
+    float r = 0.f;
+    Top2 t2 = top2_init(-1, INFINITY, INFINITY, m);
     bool pending = false;
+    if (live) pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2);
+    push_fallback(pending, task.pair, i, m, t2, queue, queue_n, queue_cap);
     if (live) {
-        double qx64, qy64, qz64;
-        transform_point(P.T, lsm_ld(S.xyz, i), qx64, qy64, qz64);
-        const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
-        // warm start: the previous pass's nearest neighbour bounds this pass's search. The search
-        // stays exact -- the (d2, index) minimum over all points does not depend on the start.
-        const int prev = corr[P.src_off + i];
-        if (prev >= 0 && prev < G.n) {
-            const float4 t = lsm_ld(G.xyz, prev);
-            const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
-            bd2 = dx * dx + dy * dy + dz * dz;
-            bidx = prev;
-        }
-        const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
-                    fz = (qz - G.oz) * G.inv_cell;
-        // a query outside the target's box searches around the nearest cell of the box: the
-        // box faces that lie on the grid boundary bound nothing (no points beyond them)
-        auto clampc = [](float f, int n) { return (int)fminf(fmaxf(floorf(f), 0.f), float(n - 1)); };
-        const int cx = clampc(fx, G.nx), cy = clampc(fy, G.ny), cz = clampc(fz, G.nz);
-        if (G.n > 0) {
-            // box half-width in cells: the warm-start radius (+ f32 slack), else NN_KCOLD
-            int K = NN_KCOLD;
-            if (bd2 < INFINITY) {
-                const float rc = sqrtf(bd2) * G.inv_cell * 1.0001f + 1e-4f;
-                K = rc >= float(NN_KMAX) ? NN_KMAX : max(1, (int)ceilf(rc));
-            }
-            const int x0 = max(cx - K, 0), x1 = min(cx + K, G.nx - 1);
-            const int y0 = max(cy - K, 0), y1 = min(cy + K, G.ny - 1);
-            const int z0 = max(cz - K, 0), z1 = min(cz + K, G.nz - 1);
-            const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
-            const uint32_t *cs = G.cell_start;
-#pragma unroll 1
-            for (int iz = 0; iz <= 2 * K; ++iz) {
-                const int dz = (iz & 1) ? -((iz + 1) >> 1) : (iz >> 1);   // 0, -1, 1, -2, 2 ...
-                const int z = cz + dz;
-                if (z < z0 || z > z1) continue;
-                const float wz = slab_cells2(fz, z) * c2;
-                if (wz >= bd2) continue;
-#pragma unroll 1
-                for (int iy = 0; iy <= 2 * K; ++iy) {
-                    const int dy = (iy & 1) ? -((iy + 1) >> 1) : (iy >> 1);
-                    const int y = cy + dy;
-                    if (y < y0 || y > y1) continue;
-                    const float wyz = wz + slab_cells2(fy, y) * c2;
-                    if (wyz >= bd2) continue;
-                    // cells of this row that can still hold a point nearer than the best
-                    int xa = x0, xb = x1;
-                    if (bd2 < INFINITY) {
-                        const float ch = sqrtf((bd2 - wyz) * 1.0002f) * G.inv_cell + 1e-4f;
-                        xa = max(xa, (int)floorf(fx - ch));
-                        xb = min(xb, (int)floorf(fx + ch));
-                    }
-                    int x = xa;
-                    while (x <= xb) {
-                        const int xe = min(xb, x | (LSM_BLK - 1));   // end of this block's row part
-                        const uint32_t a = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, x, y, z));
-                        const uint32_t b = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, xe, y, z) + 1);
-                        if (b > a) scan_run(G.xyz, a, b, qx, qy, qz, wyz, bd2, bidx);
-                        x = xe + 1;
-                    }
-                }
-            }
-            // every point outside the searched box is at least `bound` away; sides clipped by
-            // the grid hold no points.
-            const float bx = fminf(cx - K > 0 ? fx - float(cx - K) : INFINITY,
-                                   cx + K + 1 < G.nx ? float(cx + K + 1) - fx : INFINITY);
-            const float by = fminf(cy - K > 0 ? fy - float(cy - K) : INFINITY,
-                                   cy + K + 1 < G.ny ? float(cy + K + 1) - fy : INFINITY);
-            const float bz = fminf(cz - K > 0 ? fz - float(cz - K) : INFINITY,
-                                   cz + K + 1 < G.nz ? float(cz + K + 1) - fz : INFINITY);
-            const float bound = fminf(bx, fminf(by, bz)) * G.cell;
-            const float bound2 = bound * bound * 0.99999f;
-            if (bd2 <= bound2 || bound >= prm.maxc) {
-                result = (bidx >= 0 && bd2 < prm.maxc2) ? bidx : -1;
-            } else {
-                pending = true;
-            }
-        }
-    }
-    // wave-aggregated queue append
-    const uint64_t m = __ballot(pending);
-    if (m) {
-        const int lane = threadIdx.x & 63;
-        uint32_t base = 0;
-        if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(queue_n, (uint32_t)__popcll(m));
-        base = __shfl(base, __ffsll((unsigned long long)m) - 1, LSM_WAVE);
-        if (pending) {
-            const uint32_t slot = base + __popcll(m & ((uint64_t(1) << lane) - 1));
-            if (slot < queue_cap) queue[slot] = {task.pair, i, bidx, bd2};
-        }
-    }
-    if (live) {
-        const int64_t g = P.src_off + i;
         corr[g] = pending ? -2 : result;
-        corr_d2[g] = bd2;
-    }
-}
-
-__global__ void __launch_bounds__(NN_THREADS)
-nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
-          NNParams prm, int32_t *__restrict__ corr, float *__restrict__ corr_d2,
-          FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n, uint32_t queue_cap) {
-    for (int t = blockIdx.x;; t += gridDim.x) {
-        BlockTask task;
-        const int r = plan_task(tp, st, t, task);
-        if (r < 0) break;
-        if (r > 0) nn_task(task, st, cds, prm, corr, corr_d2, queue, queue_n, queue_cap);
+        rho[g] = r;
     }
 }
 
 // ------------------------------------------------------------------------------------------
 // exact fallback: one wave per unresolved query, expanding boxes (shells)
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void wave_argmin(float &d2, int &idx) {
+// (nearest, second) wave reduction; lanes holding the same point merge their second distances
+__device__ __forceinline__ void wave_top2(Top2 &t) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        const float od = __shfl_xor(d2, off, LSM_WAVE);
-        const int oi = __shfl_xor(idx, off, LSM_WAVE);
-        if (better(od, oi, d2, idx)) {
-            d2 = od;
-            idx = oi;
+        const float od = __shfl_xor(t.bd2, off, LSM_WAVE);
+        const int oi = __shfl_xor(t.bidx, off, LSM_WAVE);
+        const float os = __shfl_xor(t.sd2, off, LSM_WAVE);
+        if (oi == t.bidx) {
+            t.sd2 = fminf(t.sd2, os);
+        } else if (better(od, oi, t.bd2, t.bidx)) {
+            t.sd2 = fminf(os, t.bd2);
+            t.bd2 = od;
+            t.bidx = oi;
+        } else {
+            t.sd2 = fminf(t.sd2, od);
         }
     }
+    t.lim = prune2(t.bd2, t.sd2, t.m);
 }
 
 __device__ __forceinline__ float gap2(float q, float lo, float hi) {
@@ -368,15 +522,15 @@ __device__ __forceinline__ void ring_offset(int r, int t, int &dx, int &dy, int 
     dy = u % n2 - r + 1;
 }
 
-// Exact 1-NN for the queries the fast path could not resolve: one wave per query walks Chebyshev
-// rings of 4x4x4-cell blocks (each block one contiguous point range) outward from the query's
-// block. Lanes test 64 blocks at a time against the current best (lower-bound pruning); the
-// surviving blocks are scanned by the whole wave. Stops when every unscanned point is provably
-// farther than the best, or than max_corr.
+// Exact 1-NN for the queries the box search could not resolve: one wave per query walks
+// Chebyshev rings of 4x4x4-cell blocks (each block one contiguous point range) outward from the
+// query's block. Lanes test 64 blocks at a time against the current pruning radius
+// (prune2, lower-bound pruning); the surviving blocks are scanned by the whole wave. Stops when
+// every unscanned point is provably farther than the best, or than max_corr.
 __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
             const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
-            uint32_t queue_cap, int32_t *__restrict__ corr, float *__restrict__ corr_d2) {
+            uint32_t queue_cap, int32_t *__restrict__ corr, float *__restrict__ rho) {
     const int lane = threadIdx.x;
     const uint32_t total = min(*queue_n, queue_cap);
     for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
@@ -387,13 +541,17 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
         double qx64, qy64, qz64;
         transform_point(P.T, lsm_ld(S.xyz, q.i), qx64, qy64, qz64);
         const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
-        float bd2 = q.best_d2;
-        int bidx = q.best;
+        Top2 t2 = top2_init(q.best, q.best_d2, q.second_d2, q.margin);
         const float B = G.cell * float(LSM_BLK);
         const float gx1 = G.ox + G.nx * G.cell, gy1 = G.oy + G.ny * G.cell,
                     gz1 = G.oz + G.nz * G.cell;
         const float box2 = gap2(qx, G.ox, gx1) + gap2(qy, G.oy, gy1) + gap2(qz, G.oz, gz1);
-        if (box2 < prm.maxc2 && G.n > 0) {
+        float fbound = 0.f;   // every unscanned point is at least this far (0: unknown)
+        if (G.n <= 0) {
+            fbound = INFINITY;
+        } else if (box2 >= prm.maxc2) {
+            fbound = sqrtf(box2);   // nothing within max_corr: every point is outside the box
+        } else {
             const float invB = 1.f / B;
             const int qbx = (int)floorf((qx - G.ox) * invB), qby = (int)floorf((qy - G.oy) * invB),
                       qbz = (int)floorf((qz - G.oz) * invB);
@@ -414,7 +572,7 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
                             const float lb2 = gap2(qx, G.ox + bx * B, G.ox + (bx + 1) * B) +
                                               gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
                                               gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
-                            if (lb2 * 0.9999f < bd2) {
+                            if (lb2 * 0.9999f < t2.lim) {
                                 const int bid = (bz * G.nby + by) * G.nbx + bx;
                                 a = lsm_ld(cs, size_t(bid) * LSM_BLK_CELLS);
                                 b = lsm_ld(cs, size_t(bid + 1) * LSM_BLK_CELLS);
@@ -426,17 +584,10 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
                         const int src = __ffsll((unsigned long long)mask) - 1;
                         mask &= mask - 1;
                         const uint32_t ra = __shfl(a, src, LSM_WAVE), rb = __shfl(b, src, LSM_WAVE);
-                        for (uint32_t k = ra + lane; k < rb; k += LSM_WAVE) {
-                            const float4 t4 = lsm_ld(G.xyz, k);
-                            const float ex = qx - t4.x, ey = qy - t4.y, ez = qz - t4.z;
-                            const float d2 = ex * ex + ey * ey + ez * ez;
-                            if (better(d2, int(k), bd2, bidx)) {
-                                bd2 = d2;
-                                bidx = int(k);
-                            }
-                        }
+                        for (uint32_t k = ra + lane; k < rb; k += LSM_WAVE)
+                            top2_add(sqd(lsm_ld(G.xyz, k), qx, qy, qz), int(k), t2);
                     }
-                    wave_argmin(bd2, bidx);
+                    wave_top2(t2);
                 }
                 // every unscanned point lies outside the block cube [qb - r, qb + r]
                 float bound = INFINITY;
@@ -446,14 +597,18 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
                 if (qby + r + 1 < G.nby) bound = fminf(bound, G.oy + (qby + r + 1) * B - qy);
                 if (qbz - r > 0) bound = fminf(bound, qz - (G.oz + (qbz - r) * B));
                 if (qbz + r + 1 < G.nbz) bound = fminf(bound, G.oz + (qbz + r + 1) * B - qz);
-                if (bound == INFINITY || bd2 <= bound * bound * 0.99999f || bound >= prm.maxc)
+                if (bound == INFINITY || t2.bd2 <= bound * bound * 0.99999f ||
+                    bound >= prm.maxc) {
+                    fbound = bound;
                     break;
+                }
             }
         }
         if (lane == 0) {
             const int64_t g = P.src_off + q.i;
-            corr[g] = (bidx >= 0 && bd2 < prm.maxc2) ? bidx : -1;
-            corr_d2[g] = bd2;
+            const bool hit = t2.bidx >= 0 && t2.bd2 < prm.maxc2;
+            corr[g] = hit ? t2.bidx : -1;
+            rho[g] = hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound);
         }
     }
 }
@@ -790,7 +945,10 @@ solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NN
             for (int k = 0; k < 4; ++k) s += D[4 * r + k] * P.T[4 * k + c];
             T[4 * r + c] = s;
         }
-    for (int k = 0; k < 16; ++k) P.T[k] = T[k];
+    for (int k = 0; k < 16; ++k) {
+        P.Tp[k] = P.T[k];
+        P.T[k] = T[k];
+    }
     P.iter = pass + 1;
     P.prev_fitness = fitness;
     P.prev_rmse = rmse;
@@ -896,25 +1054,26 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     if ((rc = upload(ctx, "i_pbytes", pbytes, &d_pbytes))) return rc;
     const size_t nsrc_tot = size_t(std::max<int64_t>(src_off, 1));
     int32_t *d_corr = (int32_t *)ctx->buf("i_corr", nsrc_tot * 4);
-    float *d_cd2 = (float *)ctx->buf("i_cd2", nsrc_tot * 4);
+    float *d_rho = (float *)ctx->buf("i_rho", nsrc_tot * 4);
     const uint32_t qcap = uint32_t(nsrc_tot);
     FallbackItem *d_q = (FallbackItem *)ctx->buf("i_queue", size_t(qcap) * sizeof(FallbackItem));
     double *d_part = (double *)ctx->buf("i_part", size_t(std::max(slot, 1)) * LSM_ACC * 8);
     const int ncnt = max_iter + 2;
-    uint32_t *d_counters = (uint32_t *)ctx->buf("i_counters", size_t(ncnt) * 2 * 4);
+    uint32_t *d_counters = (uint32_t *)ctx->buf("i_counters", size_t(ncnt) * 3 * 4);
     double *d_bytes = (double *)ctx->buf("i_bytes", size_t(ncnt) * 8);
     unsigned long long *d_srcn = (unsigned long long *)ctx->buf("i_srcn", size_t(ncnt) * 8);
     int32_t *d_pref = (int32_t *)ctx->buf("i_pref", size_t(npairs + 1) * 4);
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
-    if (!d_corr || !d_cd2 || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
+    if (!d_corr || !d_rho || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
         !d_plan || !d_flags) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
     }
     uint32_t *d_qn = d_counters;            // [ncnt] fallback queue sizes per pass
     uint32_t *d_active = d_counters + ncnt; // [ncnt] active pairs after each pass
-    LSM_HIP_TRY(ctx, hipMemsetAsync(d_counters, 0, size_t(ncnt) * 2 * 4, st));
+    uint32_t *d_sqn = d_counters + 2 * ncnt; // [ncnt] uncertified queries per pass
+    LSM_HIP_TRY(ctx, hipMemsetAsync(d_counters, 0, size_t(ncnt) * 3 * 4, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_bytes, 0, size_t(ncnt) * 8, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_srcn, 0, size_t(ncnt) * 8, st));
     if (src_off > 0) LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
@@ -943,6 +1102,12 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         const char *e = getenv("LSM_PASS_LAG");
         return e ? std::max(1, atoi(e)) : 2;
     }();
+    // LSM_NN_NOCERT=1: search every query in every pass (no stability certificate) -- the
+    // tests' proof that certified passes return bit-identical correspondences
+    const char *nc_env = getenv("LSM_NN_NOCERT");
+    const bool nocert = nc_env && atoi(nc_env) != 0;
+    double ms0 = 0.0;
+    for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
     plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
     const TaskPlan tp{d_plan, d_pref, int(npairs)};
     int passes = 0, polled = 0;
@@ -965,12 +1130,16 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         if (done) break;
         hipEvent_t ev;
         ctx->tic("nn", &ev);
-        nn_kernel<<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_cd2, d_q,
-                                               d_qn + pass, qcap);
+        if (pass == 0 || nocert)
+            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_rho, d_q,
+                                                          d_qn + pass, qcap, d_sqn + pass);
+        else
+            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_rho, d_q,
+                                                         d_qn + pass, qcap, d_sqn + pass);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
         nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass, qcap, d_corr,
-                                                  d_cd2);
+                                                  d_rho);
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);
         if (p.method == LSM_P2PLANE)
@@ -1031,6 +1200,18 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     ctx->collect_timings();
     if (ctx->timing) {
         ctx->stats["nn"].algo_bytes += nn_bytes;
+        // the whole correspondence pass (check + search + fallback) of every pass
+        double ms1 = 0.0;
+        for (const char *k : {"nn", "nn_fallback"}) ms1 += ctx->stats[k].ms;
+        KStat &np = ctx->stats["nn_pass"];
+        np.launches += passes;
+        np.ms += ms1 - ms0;
+        np.algo_bytes += nn_bytes;
+        std::vector<uint32_t> sq(passes);
+        LSM_HIP_TRY(ctx, hipMemcpy(sq.data(), d_sqn, size_t(passes) * 4, hipMemcpyDeviceToHost));
+        int64_t searched = 0;
+        for (int k = 1; k < passes; ++k) searched += sq[k];
+        ctx->stats["nn_uncertified"].launches += searched;
         // search statistics: queries and the ones the fast path left to the fallback
         std::vector<uint32_t> qn(passes);
         LSM_HIP_TRY(ctx, hipMemcpy(qn.data(), d_qn, size_t(passes) * 4, hipMemcpyDeviceToHost));
@@ -1040,6 +1221,14 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         ctx->stats["nn_queries_first_pass"].launches += queries0;
         ctx->stats["nn_pending"].launches += pend;
         ctx->stats["nn_pending_first_pass"].launches += passes > 0 ? qn[0] : 0;
+        if (getenv("LSM_DEBUG_PASSES")) {   // per pass: active pairs, searched, fallback
+            std::vector<uint32_t> act(passes);
+            LSM_HIP_TRY(ctx, hipMemcpy(act.data(), d_active, size_t(passes) * 4,
+                                       hipMemcpyDeviceToHost));
+            for (int k = 0; k < passes; ++k)
+                fprintf(stderr, "pass %2d: active-after %4u  searched %8u  fallback %7u\n", k,
+                        act[k], sq[k], qn[k]);
+        }
     }
     for (int64_t k = 0; k < npairs; ++k) {
         const PairState &P = ps[k];

@@ -44,6 +44,7 @@ __host__ __device__ __forceinline__ int lsm_cell_lin(int nbx, int nby, int x, in
 // Per-pair ICP state (device). Layout kept 8-byte aligned.
 struct PairState {
     double T[16];        // current transformation (row-major), f64 as Open3D
+    double Tp[16];       // transformation of the previous correspondence pass (stability check)
     double fitness, rmse;
     double prev_fitness, prev_rmse;
     int32_t iter;        // updates applied

@@ -376,6 +376,7 @@ struct NormalParams {
     float r;          // radius (search box half-width)
     float r2_lo;      // f32 d^2 below this: certainly inside (exact f64 test not needed)
     float r2_hi;      // f32 d^2 above this: certainly outside
+    float hscale;     // f32 of the level-0 histogram scale NB8 / r^2 (see normals_kernel)
     int max_nn;
 };
 
@@ -433,6 +434,23 @@ __device__ __forceinline__ void cum_add(Cum &c, const Off &o) {
     c.sxy = fma(o.dx, o.dy, c.sxy);
     c.sxz = fma(o.dx, o.dz, c.sxz);
     c.syz = fma(o.dy, o.dz, c.syz);
+    c.n += 1;
+}
+
+// Cumulants from the exact f64 offsets of a point (f32 coordinates: the differences are exact).
+// f32 sums were tried: they move some normals by ~1e-6, which is enough to shift chaotic
+// (non-converging) registrations past the transform parity bar.
+__device__ __forceinline__ void cum_add_pt(Cum &c, float4 p, double qx, double qy, double qz) {
+    const double dx = double(p.x) - qx, dy = double(p.y) - qy, dz = double(p.z) - qz;
+    c.sx += dx;
+    c.sy += dy;
+    c.sz += dz;
+    c.sxx = fma(dx, dx, c.sxx);
+    c.syy = fma(dy, dy, c.syy);
+    c.szz = fma(dz, dz, c.szz);
+    c.sxy = fma(dx, dy, c.sxy);
+    c.sxz = fma(dx, dz, c.sxz);
+    c.syz = fma(dy, dz, c.syz);
     c.n += 1;
 }
 
@@ -604,32 +622,34 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
     float4 *nrm = const_cast<float4 *>(C.nrm);
-    // candidates in the ball's cells: when they cannot exceed max_nn, no selection is needed
-    const bool hist = true;
-    if (hist) {
 #pragma unroll
-        for (int b = 0; b < NB8 / 4; ++b) H[b] = 0;
-    }
+    for (int b = 0; b < NB8 / 4; ++b) H[b] = 0;
     Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
     bool sat = false;
     Cum c = {};
+    // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
+    // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
+    // f32 d^2 and the scale are within 4.2e-7 relative, t < 128). The rest (the sphere's
+    // rounding band, bin edges) take the exact f64 distance, so the histogram is the one the
+    // f64 binning of the later scans implies.
     ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
-            auto add = [&](const Off &o) {
-                cum_add(c, o);
-                if (hist) {
-                    const int bb = sel_level_bin(S, o.d2, k);
-                    const uint32_t v = H8[bb];
-                    sat |= v == 255u;
-                    H8[bb] = uint8_t(v + (v < 255u ? 1u : 0u));
-                }
-            };
-            const float f = f32_d2(qf, p);
-            if (f < np.r2_lo) {        // certainly inside: the common case, one branch
-                add(make_off(p, qx, qy, qz));
-            } else if (f <= np.r2_hi) {   // within f32 rounding of the sphere: exact f64 test
+            const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
+            const float f = dx * dx + dy * dy + dz * dz;
+            const float t = f * np.hscale;
+            const float fr = t - floorf(t);
+            int bb = -1;
+            if (f < np.r2_lo && fr > 2e-4f && fr < 1.f - 2e-4f) {
+                bb = int(t);
+            } else if (f <= np.r2_hi) {
                 const Off o = make_off(p, qx, qy, qz);
-                if (o.d2 < np.r2) add(o);
+                if (o.d2 < np.r2) bb = sel_level_bin(S, o.d2, k);
+            }
+            if (bb >= 0) {
+                cum_add_pt(c, p, qx, qy, qz);
+                const uint32_t v = H8[bb];
+                sat |= v == 255u;
+                H8[bb] = uint8_t(v + (v < 255u ? 1u : 0u));
             }
         });
     });
@@ -758,101 +778,6 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
         if (rank < need) cum_add(f, make_off(lsm_ld(C.xyz, ke), qx, qy, qz));
     }
     nrm[j] = normal_from_cum(f);
-}
-
-// EXPERIMENT (LSM_NORMALS_COOP=1): wave-cooperative scan 1 only (no kNN truncation).
-__device__ __forceinline__ float wave_minf(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, LSM_WAVE));
-    return v;
-}
-__device__ __forceinline__ float wave_maxf(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, LSM_WAVE));
-    return v;
-}
-__device__ __forceinline__ float bcast(float v, int i) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
-}
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-__global__ void __launch_bounds__(PT_THREADS)
-normals_coop_kernel(const Seg *segs, const CloudDev *cd, NormalParams np) {
-    const Seg s = segs[blockIdx.x];
-    const CloudDev C = cd[s.cloud];
-    const int lane = threadIdx.x & 63;
-    const int j = s.start + threadIdx.x;
-    const int j0 = s.start + (threadIdx.x & ~63);
-    if (j0 >= C.n) return;
-    const bool live = j < C.n;
-    const float4 qf = lsm_ld(C.xyz, live ? j : j0);
-    const double qx = qf.x, qy = qf.y, qz = qf.z;
-    const float r = np.r;
-    const float prune = r * 1.0001f + 1e-6f, prune2 = prune * prune;
-    const float bx0 = wave_minf(qf.x), bx1 = wave_maxf(qf.x);
-    const float by0 = wave_minf(qf.y), by1 = wave_maxf(qf.y);
-    const float bz0 = wave_minf(qf.z), bz1 = wave_maxf(qf.z);
-    auto rng = [&](float lo, float hi, float o, int n, int &a, int &b) {
-        a = max((int)floorf((lo - r - o) * C.inv_cell - 1e-3f), 0);
-        b = min((int)floorf((hi + r - o) * C.inv_cell + 1e-3f), n - 1);
-    };
-    int xlo, xhi, ylo, yhi, zlo, zhi;
-    rng(bx0, bx1, C.ox, C.nx, xlo, xhi);
-    rng(by0, by1, C.oy, C.ny, ylo, yhi);
-    rng(bz0, bz1, C.oz, C.nz, zlo, zhi);
-    Cum c = {};
-    const float *xs = reinterpret_cast<const float *>(C.xyz);
-    for (int z = zlo; z <= zhi; ++z) {
-        const float dz2 = slab_d2(qf.z, C.oz, C.cell, z);
-        for (int y = ylo; y <= yhi; ++y) {
-            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
-            const bool act = live && dyz2 <= prune2;
-            if (!__ballot(act)) continue;
-            const float ch = act ? sqrtf(prune2 - dyz2) * 1.0001f + 1e-6f * fabsf(qf.x) + 1e-5f : 0.f;
-            const float xl = wave_minf(act ? qf.x - ch : INFINITY);
-            const float xh = wave_maxf(act ? qf.x + ch : -INFINITY);
-            const int xa = max(xlo, (int)floorf((xl - C.ox) * C.inv_cell - 1e-3f));
-            const int xb = min(xhi, (int)floorf((xh - C.ox) * C.inv_cell + 1e-3f));
-            int x = xa;
-            while (x <= xb) {
-                const int xe = min(xb, x | (LSM_BLK - 1));
-                const uint32_t a = uni(lsm_ld(C.cell_start, lsm_cell_lin(C.nbx, C.nby, x, y, z)));
-                const uint32_t b = uni(lsm_ld(C.cell_start, lsm_cell_lin(C.nbx, C.nby, xe, y, z) + 1));
-                x = xe + 1;
-                if (b <= a) continue;
-                uint32_t lo = a, hi = b;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (lsm_ld(xs, size_t(mid) * 4) < xl) lo = mid + 1;
-                    else hi = mid;
-                }
-                lo = uni(lo);
-                bool stop = false;
-                for (uint32_t base = lo; base < b && !stop; base += LSM_WAVE) {
-                    const uint32_t idx = min(base + lane, b - 1);
-                    const float4 p = lsm_ld(C.xyz, idx);
-                    const int cnt = int(min(b - base, uint32_t(LSM_WAVE)));
-                    for (int i = 0; i < cnt; ++i) {
-                        const float px = bcast(p.x, i);
-                        if (px > xh) {
-                            stop = true;
-                            break;
-                        }
-                        const float py = bcast(p.y, i), pz = bcast(p.z, i);
-                        const float dx = qf.x - px, dy = qf.y - py, dz = qf.z - pz;
-                        const float f = dx * dx + dy * dy + dz * dz;
-                        const bool maybe = act && f <= np.r2_hi;
-                        if (!__ballot(maybe)) continue;
-                        if (maybe) {
-                            const Off o = make_off(make_float4(px, py, pz, 0.f), qx, qy, qz);
-                            if (f < np.r2_lo || o.d2 < np.r2) cum_add(c, o);
-                        }
-                    }
-                }
-            }
-        }
-    }
-    if (live) const_cast<float4 *>(C.nrm)[j] = normal_from_cum(c);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1307,12 +1232,9 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         np.r = float(p.normal_radius);
         np.r2_lo = float(np.r2 * (1.0 - 4e-6));
         np.r2_hi = float(np.r2 * (1.0 + 4e-6));
+        np.hscale = float(double(NB8) / np.r2);
         np.max_nn = p.max_nn;
         ctx->tic("normals", &ev);
-        static const bool coop = getenv("LSM_NORMALS_COOP") != nullptr;
-        if (coop)
-            normals_coop_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np);
-        else
         {
             static const bool nstats = getenv("LSM_NORMALS_STATS") != nullptr;
             unsigned long long *d_ns = nullptr;

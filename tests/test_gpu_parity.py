@@ -260,3 +260,38 @@ def test_loop_candidates_bit_exact(dev):
             trip = O.find_feasible_triplets(P[:m], m - 1, cand)
             got = [[m - 1, int(j1), int(j2)] for j1, j2 in zip(cand, part) if j2 >= 0]
             assert got == trip
+
+
+# ------------------------------------------------------------------ stability certificate (a6.1)
+@pytest.mark.parametrize("method,max_corr", [("p2plane", 10.0), ("p2p", 10.0), ("p2plane", 0.5)])
+def test_certified_passes_bit_identical(dev, method, max_corr, monkeypatch):
+    """Passes >= 1 skip the search for queries whose neighbour is certified unchanged
+    (nn_check_kernel). The certificate only claims what a full search would return, so every
+    result must be bit-identical to LSM_NN_NOCERT=1 (every query searched in every pass) --
+    including the none-within-max_corr queries a small max_corr produces."""
+    seq = synthetic.make_sequence(4, seed=7, model=synthetic.HDL64)
+    ids = _prep(dev, seq.scans, want_normals=(method == "p2plane"))
+    try:
+        prm = _lib.icp_params(method=method, max_correspondence_distance=max_corr)
+        src, tgt = ids[1:], ids[:-1]
+        dev.reset_stats()
+        dev.set_timing(True)
+        cert = dev.icp_batch(src, tgt, seq.priors, prm)
+        c_cert = dev.last_correspondences()
+        dev.set_timing(False)
+        queried = dev.kernel_stats("nn_queries")["launches"]
+        searched = dev.kernel_stats("nn_uncertified")["launches"]
+        monkeypatch.setenv("LSM_NN_NOCERT", "1")
+        full = dev.icp_batch(src, tgt, seq.priors, prm)
+        c_full = dev.last_correspondences()
+        monkeypatch.delenv("LSM_NN_NOCERT")
+        for a, b in zip(cert, full):
+            assert np.array_equal(a["transformation"], b["transformation"])
+            assert a["fitness"] == b["fitness"] and a["inlier_rmse"] == b["inlier_rmse"]
+            assert a["iterations"] == b["iterations"] and a["n_corr"] == b["n_corr"]
+        assert np.array_equal(c_cert, c_full)
+        first = sum(dev.info(i)[1] for i in src)
+        # the certificate must actually carry the later passes (P2P creeps: weaker)
+        assert searched < (0.5 if method == "p2plane" else 0.9) * (queried - first)
+    finally:
+        _release(dev, ids)
