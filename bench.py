@@ -36,8 +36,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs-per-gpu", type=int, default=256)
-    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--workload", default="hdl64_seq", choices=["hdl64_seq", "ouster_multiscale"],
+                    help="hdl64_seq: C2/C3 64k HDL-64 sequence pairs (the headline line); "
+                         "ouster_multiscale: C5 256k Ouster-128, voxel 0.4/0.2/0.1 m chain")
+    ap.add_argument("--pairs-per-gpu", type=int, default=0, help="0: 256 (hdl64), 32 (ouster)")
+    ap.add_argument("--seed", type=int, default=-1, help="-1: 3 (hdl64), 5 (ouster)")
     ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
     ap.add_argument("--cpu-sample-pairs", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -66,6 +69,21 @@ def cpu_baseline(seq, n_pairs: int, method: str, threads: int):
                       f"{dt:.1f} s"}
 
 
+def cpu_baseline_multiscale(seq, n_pairs: int, method: str, threads: int):
+    """The f64 oracle's multi-scale chain on the first n_pairs pairs of the same data."""
+    from oracle import open3d_restated as O
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    O.WORKERS = threads
+    t0 = time.perf_counter()
+    for k in range(n_pairs):
+        O.registration_multiscale(seq.scans[k + 1], seq.scans[k], seq.priors[k], method=method)
+    dt = time.perf_counter() - t0
+    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n_pairs} pair(s) of the same Ouster-128 sequence through the 3-scale "
+                      f"chain (both keyframes pre-processed per pair), f64 NumPy/SciPy oracle, "
+                      f"{dt:.1f} s"}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -83,21 +101,40 @@ def main():
     from lidar_slam_arvc_amd import _lib, synthetic
     from lidar_slam_arvc_amd.distributed import compose_global_sharded
 
-    P = args.pairs_per_gpu
+    ouster = args.workload == "ouster_multiscale"
+    P = args.pairs_per_gpu or (32 if ouster else 256)
     first = rank * P
-    seq = synthetic.make_sequence(P + 1, seed=args.seed, model=synthetic.HDL64, first_index=first)
+    model = synthetic.OUSTER128 if ouster else synthetic.HDL64
+    seed = args.seed if args.seed >= 0 else (5 if ouster else 3)
+    seq = synthetic.make_sequence(P + 1, seed=seed, model=model, first_index=first)
     dev = _lib.device(local)
     ids = [dev.upload(s) for s in seq.scans]        # raw scans resident in HBM
-    prep = _lib.prep_params(want_normals=(args.method == "p2plane"), grid_cell=args.grid_cell)
-    icp = _lib.icp_params(method=args.method)
+    want_normals = args.method == "p2plane"
     cuda = torch.device("cuda", local)
+    ms = None
+    if ouster:
+        from lidar_slam_arvc_amd.multiscale import MultiScaleSet
+        ms = MultiScaleSet(dev, ids)                 # per-scale device clones, made once
 
-    def step():
-        n = dev.preprocess(ids, prep)
-        res = dev.icp_batch(ids[1:], ids[:-1], seq.priors, icp)
-        rel = np.stack([r["transformation"] for r in res])
-        compose_global_sharded(rel, group=group, device=cuda)
-        return n, res
+        def step():
+            ms.preprocess(want_normals=want_normals, grid_cell=args.grid_cell)
+            stages = ms.register(list(range(1, P + 1)), list(range(P)), seq.priors,
+                                 method=args.method)
+            res = stages[-1]
+            rel = np.stack([r["transformation"] for r in res])
+            compose_global_sharded(rel, group=group, device=cuda)
+            n = [dev.info(h)[1] for h in ms.handles[-1]]
+            return n, res
+    else:
+        prep = _lib.prep_params(want_normals=want_normals, grid_cell=args.grid_cell)
+        icp = _lib.icp_params(method=args.method)
+
+        def step():
+            n = dev.preprocess(ids, prep)
+            res = dev.icp_batch(ids[1:], ids[:-1], seq.priors, icp)
+            rel = np.stack([r["transformation"] for r in res])
+            compose_global_sharded(rel, group=group, device=cuda)
+            return n, res
 
     for _ in range(args.warmup):
         step()
@@ -129,7 +166,7 @@ def main():
         achieved = nn["algo_bytes"] / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "nn_traffic.json")
-        if os.path.exists(tfile):
+        if os.path.exists(tfile) and not ouster:
             with open(tfile) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -143,10 +180,13 @@ def main():
                                            for k in ("nn", "nn_fallback")}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(seq, args.cpu_sample_pairs, args.method, args.cpu_threads)
+            cpu = (cpu_baseline_multiscale(seq, max(1, args.cpu_sample_pairs // 2), args.method,
+                                           args.cpu_threads) if ouster else
+                   cpu_baseline(seq, args.cpu_sample_pairs, args.method, args.cpu_threads))
         ms_step = dt / args.steps * 1e3
         out = {
-            "metric": "ICP keyframe-pair registrations/sec (64k-pt scans)",
+            "metric": ("ICP keyframe-pair registrations/sec (256k-ray Ouster-128, multi-scale)"
+                       if ouster else "ICP keyframe-pair registrations/sec (64k-pt scans)"),
             "value": round(world * P * args.steps / dt, 3),
             "unit": "pairs/s",
             "n_gpus": world,
@@ -157,24 +197,32 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32+f64",
-            "data": "synthetic (seeded ray-cast HDL-64 scans of a procedural scene)",
-            "config": {"workload": "hdl64_64k_p2plane_seq" if args.method == "p2plane"
-                       else "hdl64_64k_p2p_seq",
-                       "pairs_per_gpu": P, "global_pairs": world * P,
-                       "points_per_scan_post_filter": int(np.mean(n_pts)),
-                       "rays_per_scan": 65536, "method": args.method,
-                       "max_correspondence_distance": 10.0,
-                       "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"},
+            "data": "synthetic (seeded ray-cast %s scans of a procedural scene)"
+                    % ("Ouster-128" if ouster else "HDL-64"),
+            "config": ({"workload": f"ouster128_256k_{args.method}_multiscale_seq",
+                        "pairs_per_gpu": P, "global_pairs": world * P,
+                        "points_per_scan_finest_voxel": int(np.mean(n_pts)),
+                        "rays_per_scan": 262144, "method": args.method,
+                        "voxel_scales": [0.4, 0.2, 0.1],
+                        "max_correspondence_distance": [2.0, 1.0, 0.5],
+                        "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"}
+                       if ouster else
+                       {"workload": f"hdl64_64k_{args.method}_seq",
+                        "pairs_per_gpu": P, "global_pairs": world * P,
+                        "points_per_scan_post_filter": int(np.mean(n_pts)),
+                        "rays_per_scan": 65536, "method": args.method,
+                        "max_correspondence_distance": 10.0,
+                        "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"}),
             "roofline": roof,
             "cpu_baseline": cpu,
             "mean_icp_iterations": float(np.mean(iters)),
             "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
                                       for k, v in stats.items() if v["launches"]},
             "nn_uncertified_fraction_after_pass0": round(
-            dev.kernel_stats("nn_uncertified")["launches"] /
-            max(dev.kernel_stats("nn_queries")["launches"] -
-                dev.kernel_stats("nn_queries_first_pass")["launches"], 1), 5),
-        "nn_fallback_fraction": {
+                dev.kernel_stats("nn_uncertified")["launches"] /
+                max(dev.kernel_stats("nn_queries")["launches"] -
+                    dev.kernel_stats("nn_queries_first_pass")["launches"], 1), 5),
+            "nn_fallback_fraction": {
                 "all_passes": round(dev.kernel_stats("nn_pending")["launches"] /
                                     max(dev.kernel_stats("nn_queries")["launches"], 1), 5),
                 "first_pass": round(dev.kernel_stats("nn_pending_first_pass")["launches"] /
@@ -184,6 +232,8 @@ def main():
     if group is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if ms is not None:
+        ms.release()
     for i in ids:
         dev.release(i)
 

@@ -91,6 +91,11 @@ void lsm_default_icp_params(lsm_icp_params *p);
 int lsm_cloud_upload(lsm_ctx *ctx, const float *xyz, int64_t n, lsm_cloud *out);
 /* Same from float64 (rounded to float32 on the device hot path). */
 int lsm_cloud_upload_f64(lsm_ctx *ctx, const double *xyz, int64_t n, lsm_cloud *out);
+/* A second handle on a device copy of src's raw points (no host round trip), for processing one
+ * scan at several settings at once: the multi-scale chain of config C5
+ * keeps one voxelised cloud per scale, where the reference would call voxel_down_sample on
+ * copies of pointcloud (keyframe.py:150-151). */
+int lsm_cloud_clone(lsm_ctx *ctx, lsm_cloud src, lsm_cloud *out);
 /* KeyFrame.unload_pointcloud (keyframe.py:61-72): frees the device buffers of the handle. */
 int lsm_cloud_release(lsm_ctx *ctx, lsm_cloud cloud);
 /* n_raw: uploaded points; n_proc: points after pre-processing (0 before); has_normals. */

@@ -21,7 +21,7 @@ LSM_P2PLANE = 1
 
 EXPORTED = [
     "lsm_init", "lsm_free", "lsm_last_error", "lsm_version", "lsm_default_prep_params",
-    "lsm_default_icp_params", "lsm_cloud_upload", "lsm_cloud_upload_f64", "lsm_cloud_release",
+    "lsm_default_icp_params", "lsm_cloud_upload", "lsm_cloud_upload_f64", "lsm_cloud_clone", "lsm_cloud_release",
     "lsm_cloud_info", "lsm_preprocess", "lsm_preprocess_batch", "lsm_cloud_download",
     "lsm_cloud_voxel_keys", "lsm_icp", "lsm_icp_batch", "lsm_icp_last_correspondences",
     "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
@@ -70,6 +70,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "lsm_default_icp_params": (None, [C.POINTER(IcpParams)]),
         "lsm_cloud_upload": (C.c_int, [_P, _f32p, C.c_int64, _i64p]),
         "lsm_cloud_upload_f64": (C.c_int, [_P, _f64p, C.c_int64, _i64p]),
+        "lsm_cloud_clone": (C.c_int, [_P, C.c_int64, _i64p]),
         "lsm_cloud_release": (C.c_int, [_P, C.c_int64]),
         "lsm_cloud_info": (C.c_int, [_P, C.c_int64, _i64p, _i64p, _i32p]),
         "lsm_preprocess": (C.c_int, [_P, C.c_int64, C.POINTER(PrepParams), _i64p]),
@@ -155,6 +156,12 @@ class Device:
             p = np.ascontiguousarray(p, dtype=np.float64)
             self.check(self.lib.lsm_cloud_upload_f64(self.handle, _ptr(p, C.c_double), len(p),
                                                      C.byref(out)), "lsm_cloud_upload_f64")
+        return out.value
+
+    def clone(self, cloud: int) -> int:
+        out = C.c_int64()
+        self.check(self.lib.lsm_cloud_clone(self.handle, int(cloud), C.byref(out)),
+                   "lsm_cloud_clone")
         return out.value
 
     def release(self, cloud: int):

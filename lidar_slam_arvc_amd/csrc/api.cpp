@@ -217,6 +217,32 @@ int lsm_cloud_upload_f64(lsm_ctx *ctx, const double *xyz, int64_t n, lsm_cloud *
     return upload_common(ctx, xyz, n, true, out);
 }
 
+int lsm_cloud_clone(lsm_ctx *ctx, lsm_cloud src, lsm_cloud *out) {
+    if (!ctx || !out) return LSM_EINVAL;
+    Cloud *s = find_cloud(ctx, src);
+    if (!s) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    (void)hipSetDevice(ctx->device);
+    Cloud *c = new Cloud();
+    c->n_raw = s->n_raw;
+    const size_t bytes = size_t(s->n_raw > 0 ? s->n_raw : 1) * 3 * sizeof(float);
+    if (hipMalloc(&c->d_raw, bytes) != hipSuccess) {
+        delete c;
+        ctx->set_error("hipMalloc failed for raw cloud");
+        return LSM_ENOMEM;
+    }
+    if (s->n_raw > 0)
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_raw, s->d_raw, size_t(s->n_raw) * 12,
+                                        hipMemcpyDeviceToDevice, ctx->stream));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const int64_t id = ctx->next_id++;
+    ctx->clouds[id] = c;
+    *out = id;
+    return LSM_OK;
+}
+
 int lsm_cloud_release(lsm_ctx *ctx, lsm_cloud cloud) {
     if (!ctx) return LSM_EINVAL;
     Cloud *c = find_cloud(ctx, cloud);

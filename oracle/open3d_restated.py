@@ -482,3 +482,25 @@ def compose_global(relative, T0=None):
         T = T @ R
         out.append(T)
     return np.asarray(out)
+
+
+# --------------------------------------------------------------------------------------------
+# C5 multi-scale chain: KeyFrame.pre_process with voxel_size (keyframe.py:156-162: filter ->
+# voxel_down_sample -> estimate_normals) and local_registration_simple (keyframe.py:231-260),
+# repeated coarse to fine with each stage initialised by the previous stage's transform.
+# --------------------------------------------------------------------------------------------
+def registration_multiscale(source_raw, target_raw, init=None, scales=(0.4, 0.2, 0.1),
+                            max_corr=(2.0, 1.0, 0.5), method="p2plane"):
+    """Returns the per-stage registration_icp results (the last one is the answer)."""
+    src_f = filter_radius_height(source_raw)
+    tgt_f = filter_radius_height(target_raw)
+    T = np.eye(4) if init is None else np.array(init, dtype=np.float64)
+    out = []
+    for v, d in zip(scales, max_corr):
+        src = voxel_down_sample(src_f, v)[1]
+        tgt = voxel_down_sample(tgt_f, v)[1]
+        nrm = estimate_normals(tgt) if method == "p2plane" else None
+        r = registration_icp(src, tgt, d, T, method, nrm)
+        T = r["transformation"]
+        out.append(r)
+    return out

@@ -295,3 +295,42 @@ def test_certified_passes_bit_identical(dev, method, max_corr, monkeypatch):
         assert searched < (0.5 if method == "p2plane" else 0.9) * (queried - first)
     finally:
         _release(dev, ids)
+
+
+# ------------------------------------------------------------------ multi-scale chain (C5)
+@pytest.mark.parametrize("method", ["p2plane", "p2p"])
+def test_multiscale_ouster_pair(dev, method):
+    """C5: a 256k-ray Ouster-128 pair through voxel scales 0.4 / 0.2 / 0.1 m (max_corr 2 / 1 /
+    0.5 m), every stage checked against the oracle's own chain."""
+    from lidar_slam_arvc_amd.multiscale import register_multiscale
+    seq = synthetic.make_sequence(2, seed=5, model=synthetic.OUSTER128)
+    ids = [dev.upload(s) for s in seq.scans]
+    try:
+        final, stages = register_multiscale(dev, [ids[1]], [ids[0]], seq.priors[:1],
+                                            method=method, return_stages=True)
+        ref = O.registration_multiscale(seq.scans[1], seq.scans[0], seq.priors[0],
+                                        method=method)
+        assert len(stages) == len(ref) == 3
+        for got, r in zip(stages, ref):
+            T, R = got[0]["transformation"], r["transformation"]
+            assert np.abs(T[:3, :3] - R[:3, :3]).max() < R_TOL
+            assert np.abs(T[:3, 3] - R[:3, 3]).max() < T_TOL
+            assert abs(got[0]["fitness"] - r["fitness"]) < 1e-3
+        # the chain lands on the ground-truth relative pose (synthetic scans)
+        gt = np.linalg.inv(seq.poses[0]) @ seq.poses[1]
+        assert np.abs(final[0]["transformation"][:3, 3] - gt[:3, 3]).max() < 0.05
+    finally:
+        _release(dev, ids)
+
+
+def test_clone_is_independent(dev, seq8k):
+    a = dev.upload(seq8k.scans[0])
+    b = dev.clone(a)
+    try:
+        dev.preprocess([a], _lib.prep_params(want_normals=False))
+        dev.preprocess([b], _lib.prep_params(want_normals=False, voxel_size=0.25))
+        assert np.array_equal(dev.download(a), O.filter_radius_height(seq8k.scans[0]))
+        ref = O.voxel_down_sample(O.filter_radius_height(seq8k.scans[0]), 0.25)[1]
+        assert np.array_equal(dev.download(b), ref)
+    finally:
+        _release(dev, [a, b])
