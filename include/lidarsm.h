@@ -129,6 +129,24 @@ int lsm_icp_batch(lsm_ctx *ctx, int64_t npairs, const lsm_cloud *src, const lsm_
  * as (source index, target index) pairs in reference order. Returns the count in *n. */
 int lsm_icp_last_correspondences(lsm_ctx *ctx, int64_t *pairs, int64_t cap, int64_t *n);
 
+/* 'icp2planes' pre-processing --------------------------------------
+ * KeyFrame.calculate_plane (keyframe.py:417-437): RANSAC plane (Open3D PointCloud.segment_plane
+ * restated: ransac_n = 3, inliers |plane . (p, 1)| <= distance_threshold, best by count then
+ * error / sqrt(count), probability-based early stop, least-squares refit of the winner's
+ * inliers) over the processed cloud's points with z < height. The candidate samples come from
+ * splitmix64(seed) (lsm_plane_samples; the reference's Open3D RNG is unseeded). Fails with
+ * LSM_EINVAL when fewer than 3 points lie below `height` (Open3D's LogError). */
+int lsm_ground_plane(lsm_ctx *ctx, lsm_cloud cloud, double height, double distance_threshold,
+                     int64_t num_iterations, uint64_t seed, double probability, double plane[4],
+                     int64_t *n_inliers, int64_t *n_subset);
+/* The three distinct subset indices of every RANSAC candidate: out = num_iterations x 3. */
+int lsm_plane_samples_get(uint64_t seed, int64_t n, int64_t num_iterations, int32_t *out);
+/* KeyFrame.segment_plane (keyframe.py:439-461): |a x + b y + c z + d| / |(a, b, c)| < threshold
+ * -> *ground, else -> *rest: two NEW raw clouds (reference order, as select_by_index) to be
+ * pre-processed (normals) like uploads. */
+int lsm_split_plane(lsm_ctx *ctx, lsm_cloud cloud, const double plane[4], double threshold,
+                    lsm_cloud *ground, lsm_cloud *rest);
+
 /* Loop-closure candidate matching (graphslam/loopclosing.py:102-144, :202-268) -------------
  * positions: m x 3 float64 trajectory (store_positions :202-211, last row = current pose).
  * index_backwards: find_index_backwards :223-237 (-1 for None).

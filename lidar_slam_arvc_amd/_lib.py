@@ -25,7 +25,7 @@ EXPORTED = [
     "lsm_cloud_info", "lsm_preprocess", "lsm_preprocess_batch", "lsm_cloud_download",
     "lsm_cloud_voxel_keys", "lsm_icp", "lsm_icp_batch", "lsm_icp_last_correspondences",
     "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
-    "lsm_reset_stats",
+    "lsm_reset_stats", "lsm_ground_plane", "lsm_plane_samples_get", "lsm_split_plane",
 ]
 
 
@@ -88,6 +88,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "lsm_set_timing": (C.c_int, [_P, C.c_int32]),
         "lsm_kernel_stats": (C.c_int, [_P, C.c_char_p, _i64p, _f64p, _f64p]),
         "lsm_reset_stats": (C.c_int, [_P]),
+        "lsm_ground_plane": (C.c_int, [_P, C.c_int64, C.c_double, C.c_double, C.c_int64,
+                                       C.c_uint64, C.c_double, _f64p, _i64p, _i64p]),
+        "lsm_plane_samples_get": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, _i32p]),
+        "lsm_split_plane": (C.c_int, [_P, C.c_int64, _f64p, C.c_double, _i64p, _i64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -106,6 +110,16 @@ def lib() -> C.CDLL:
         if _lib is None:
             _lib = load_library()
         return _lib
+
+
+def plane_samples(seed: int, n: int, num_iterations: int) -> np.ndarray:
+    """The RANSAC candidate samples lsm_ground_plane draws (num_iterations x 3 indices)."""
+    out = np.zeros((int(num_iterations), 3), dtype=np.int32)
+    rc = lib().lsm_plane_samples_get(int(seed) & 0xFFFFFFFFFFFFFFFF, int(n), int(num_iterations),
+                                     _ptr(out, C.c_int32))
+    if rc != LSM_OK:
+        raise ValueError("plane_samples needs n >= 3")
+    return out
 
 
 def _ptr(a: np.ndarray, ct):
@@ -163,6 +177,27 @@ class Device:
         self.check(self.lib.lsm_cloud_clone(self.handle, int(cloud), C.byref(out)),
                    "lsm_cloud_clone")
         return out.value
+
+    def ground_plane(self, cloud: int, height=-0.5, distance_threshold=0.01,
+                     num_iterations=1000, seed=0, probability=0.99999999):
+        """KeyFrame.calculate_plane on the device: (plane[4], n_inliers, n_subset)."""
+        plane = np.zeros(4)
+        ni, ns = C.c_int64(), C.c_int64()
+        self.check(self.lib.lsm_ground_plane(self.handle, int(cloud), float(height),
+                                             float(distance_threshold), int(num_iterations),
+                                             int(seed) & 0xFFFFFFFFFFFFFFFF, float(probability),
+                                             _ptr(plane, C.c_double), C.byref(ni), C.byref(ns)),
+                   "segment_plane")
+        return plane, ni.value, ns.value
+
+    def split_plane(self, cloud: int, plane, threshold=0.4):
+        """KeyFrame.segment_plane on the device: two new raw cloud handles (ground, rest)."""
+        pl = np.ascontiguousarray(plane, dtype=np.float64)
+        g, r = C.c_int64(), C.c_int64()
+        self.check(self.lib.lsm_split_plane(self.handle, int(cloud), _ptr(pl, C.c_double),
+                                            float(threshold), C.byref(g), C.byref(r)),
+                   "lsm_split_plane")
+        return g.value, r.value
 
     def release(self, cloud: int):
         self.check(self.lib.lsm_cloud_release(self.handle, int(cloud)), "lsm_cloud_release")

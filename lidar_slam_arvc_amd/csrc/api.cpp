@@ -243,6 +243,66 @@ int lsm_cloud_clone(lsm_ctx *ctx, lsm_cloud src, lsm_cloud *out) {
     return LSM_OK;
 }
 
+int lsm_ground_plane(lsm_ctx *ctx, lsm_cloud cloud, double height, double distance_threshold,
+                     int64_t num_iterations, uint64_t seed, double probability, double plane[4],
+                     int64_t *n_inliers, int64_t *n_subset) {
+    if (!ctx || !plane) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!c->processed) {
+        ctx->set_error("cloud not pre-processed");
+        return LSM_ESTATE;
+    }
+    if (!(probability > 0.0 && probability <= 1.0)) {
+        ctx->set_error("Probability must be > 0 or <= 1.0");
+        return LSM_EINVAL;
+    }
+    if (num_iterations < 1 || num_iterations > (int64_t(1) << 24) || !(distance_threshold >= 0)) {
+        ctx->set_error("invalid RANSAC parameters");
+        return LSM_EINVAL;
+    }
+    (void)hipSetDevice(ctx->device);
+    return lsm_ground_plane_run(ctx, c, height, distance_threshold, num_iterations, seed,
+                                probability, plane, n_inliers, n_subset);
+}
+
+int lsm_plane_samples_get(uint64_t seed, int64_t n, int64_t num_iterations, int32_t *out) {
+    if (n < 3 || num_iterations < 0 || (num_iterations > 0 && !out)) return LSM_EINVAL;
+    lsm_plane_samples(seed, n, num_iterations, out);
+    return LSM_OK;
+}
+
+int lsm_split_plane(lsm_ctx *ctx, lsm_cloud cloud, const double plane[4], double threshold,
+                    lsm_cloud *ground, lsm_cloud *rest) {
+    if (!ctx || !plane || !ground || !rest) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!c->processed) {
+        ctx->set_error("cloud not pre-processed");
+        return LSM_ESTATE;
+    }
+    (void)hipSetDevice(ctx->device);
+    Cloud *g = new Cloud(), *r = new Cloud();
+    const int rc = lsm_split_plane_run(ctx, c, plane, threshold, g, r);
+    if (rc != LSM_OK) {
+        free_cloud(g);
+        free_cloud(r);
+        return rc;
+    }
+    const int64_t ig = ctx->next_id++, ir = ctx->next_id++;
+    ctx->clouds[ig] = g;
+    ctx->clouds[ir] = r;
+    *ground = ig;
+    *rest = ir;
+    return LSM_OK;
+}
+
 int lsm_cloud_release(lsm_ctx *ctx, lsm_cloud cloud) {
     if (!ctx) return LSM_EINVAL;
     Cloud *c = find_cloud(ctx, cloud);

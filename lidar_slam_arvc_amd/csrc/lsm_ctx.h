@@ -95,3 +95,9 @@ int lsm_loop_candidates_run(lsm_ctx *ctx, const double *positions, int64_t m, do
 int lsm_loop_partners_run(lsm_ctx *ctx, const double *positions, int64_t m,
                           const int64_t *cand, int64_t ncand, int64_t *partner);
 int lsm_download_run(lsm_ctx *ctx, Cloud *c, double *xyz, double *nrm, int64_t cap);
+int lsm_ground_plane_run(lsm_ctx *ctx, Cloud *c, double height, double thr, int64_t iters,
+                         uint64_t seed, double probability, double plane[4], int64_t *n_inliers,
+                         int64_t *n_subset);
+int lsm_split_plane_run(lsm_ctx *ctx, Cloud *c, const double plane[4], double thr, Cloud *g,
+                        Cloud *r);
+void lsm_plane_samples(uint64_t seed, int64_t n, int64_t iters, int32_t *out);

@@ -8,14 +8,19 @@ behind them are replaced by liblidarsm (include/lidarsm.h) through ctypes:
     down_sample                keyframe.py:108-111  lsm_preprocess (filter + voxel)
     pre_process                keyframe.py:113-124  lsm_preprocess (filter + voxel + normals)
     local_registration_simple  keyframe.py:231-260  lsm_icp (P2P / P2Plane, Open3D criteria)
+    preprocess_icp2planes      keyframe.py:164-189  lsm_ground_plane (RANSAC) + lsm_split_plane +
+                                                    normals of both parts
+    local_registration_two_planes keyframe.py:262-295  two P2Plane ICPs in one batch, composed
 
 ``pointcloud`` / ``pointcloud_filtered`` expose ``.points`` (N x 3 float64) and ``.normals`` like
 the o3d.geometry.PointCloud the reference kept, downloaded lazily from the device cache.
 
 Deliberate divergences: an unknown ``option`` raises ValueError (the
-reference hits UnboundLocalError, keyframe.py:253-255); 'icp2planes' and 'fpfh' pre-processing
-(keyframe.py:164-229) raise NotImplementedError; ``transform`` returns a
-transformed host copy instead of mutating the device-resident filtered cloud.
+reference hits UnboundLocalError, keyframe.py:253-255); 'fpfh' pre-processing (keyframe.py:191-229)
+raises NotImplementedError; ``transform`` returns a transformed host copy
+instead of mutating the device-resident filtered cloud; the RANSAC of 'icp2planes' samples from
+splitmix64(``ransac_seed``) where Open3D uses its unseeded RNG, and ``segment_plane`` returns the
+two parts with their final normals (r = 0.5 ground / 0.3 rest) already estimated.
 """
 from __future__ import annotations
 
@@ -120,6 +125,8 @@ class KeyFrame:
         self._source = None           # path or "memory" of the resident raw cloud
         self._filter = None           # (radii, heights) of the current filtered cloud
         self._prep_key = None         # parameters of the current processed cloud
+        self._planes = None           # (ground, rest) device handles of 'icp2planes'
+        self.ransac_seed = 0          # RANSAC sampler seed (calculate_plane)
 
     # ------------------------------------------------------------------ raw cloud
     def pcd_path(self):
@@ -150,7 +157,16 @@ class KeyFrame:
                 self._handle = None
                 self._source = None
 
+    def _release_planes(self):
+        if self._planes is not None:
+            try:
+                for h in self._planes:
+                    self._dev.release(h)
+            finally:
+                self._planes = None
+
     def unload_pointcloud(self):
+        self._release_planes()
         self._release()
         self.pointcloud = None
         self.pointcloud_filtered = None
@@ -161,6 +177,7 @@ class KeyFrame:
 
     def __del__(self):
         try:
+            self._release_planes()
             self._release()
         except Exception:
             pass
@@ -208,9 +225,54 @@ class KeyFrame:
             self.preprocess_icp_point_point()
         elif method == "icppointplane":
             self.preprocess_icp_point_plane()
-        elif method in ("icp2planes", "fpfh"):
-            raise NotImplementedError(f"pre-processing method {method!r} is not on the MI355X "
-                                      "path yet (SURVEY.md §8f)")
+        elif method == "icp2planes":
+            self.preprocess_icp2planes()
+        elif method == "fpfh":
+            raise NotImplementedError("pre-processing method 'fpfh' is not on the MI355X path "
+                                      "yet (SURVEY.md §8f row 4)")
+
+    # ------------------------------------------------------------------ two planes (§8f row 2)
+    def preprocess_icp2planes(self):
+        self._run(None, None, self.voxel_size, True)
+        self.plane_model = self.calculate_plane(pcd=self.pointcloud_filtered)
+        g, ng = self.segment_plane(self.plane_model, pcd=self.pointcloud_filtered)
+        self.pointcloud_ground_plane = g
+        self.pointcloud_non_ground_plane = ng
+
+    def calculate_plane(self, pcd=None, height=-0.5, thresholdA=0.01):
+        """RANSAC ground plane [a, b, c, d] of the points below `height` (keyframe.py:417-437)."""
+        if pcd is not None and getattr(pcd, "_handle", self._handle) != self._handle:
+            raise ValueError("calculate_plane works on this keyframe's device cloud")
+        if self._handle is None or self._prep_key is None:
+            raise RuntimeError("calculate_plane needs a pre-processed keyframe")
+        plane, _, _ = self._dev.ground_plane(self._handle, height, thresholdA, 1000,
+                                             seed=self.ransac_seed)
+        return plane.tolist()
+
+    def segment_plane(self, plane_model, pcd=None, thresholdB=0.4):
+        """(ground, non-ground) clouds within / beyond thresholdB of the plane
+        (keyframe.py:439-461), resident on the device with their normals."""
+        if pcd is not None and getattr(pcd, "_handle", self._handle) != self._handle:
+            raise ValueError("segment_plane works on this keyframe's device cloud")
+        self._release_planes()
+        g, ng = self._dev.split_plane(self._handle, np.asarray(plane_model, dtype=np.float64),
+                                      thresholdB)
+        self._planes = (g, ng)
+        keep_all = dict(min_radius=0.0, max_radius=1e15, min_height=-1e15, max_height=1e15,
+                        max_nn=ICP_PARAMETERS.max_nn_gd, want_normals=True)
+        self._dev.preprocess([g], _lib.prep_params(normal_radius=self.voxel_size_normals_ground_plane,
+                                                   **keep_all))
+        keep_all["max_nn"] = ICP_PARAMETERS.max_nn
+        self._dev.preprocess([ng], _lib.prep_params(normal_radius=self.voxel_size_normals,
+                                                    **keep_all))
+        return DevicePointCloud(self._dev, g, True), DevicePointCloud(self._dev, ng, True)
+
+    def local_registration_two_planes(self, other, initial_transform):
+        """Ground parts and non-ground parts registered from the same guess (one ICP batch);
+        x, y, yaw from the non-ground result, z, roll, pitch from the ground result."""
+        T, _ = two_planes_batch(self._dev, [(self, other)],
+                                [np.eye(4) if initial_transform is None else initial_transform])
+        return T[0]
 
     # ------------------------------------------------------------------ registration
     def registration_params(self, option):
@@ -239,3 +301,33 @@ class KeyFrame:
         pc = self.pointcloud_filtered
         host = pc.to_host() if isinstance(pc, DevicePointCloud) else pc
         return host.transform(T)
+
+
+def two_planes_batch(dev, pairs, inits):
+    """local_registration_two_planes for many (target, source) keyframe pairs: all 2P ICPs in one
+    device batch. Returns (HomogeneousMatrix list, raw per-pair (ground, rest) results)."""
+    from .se3 import Euler
+    src, tgt, init = [], [], []
+    for (kt, ks), T0 in zip(pairs, inits):
+        for kf in (kt, ks):
+            if kf._planes is None:
+                raise RuntimeError("local_registration_two_planes needs "
+                                   "pre_process('icp2planes') on both keyframes")
+        T0 = np.asarray(getattr(T0, "array", T0), dtype=np.float64).reshape(16)
+        src += [ks._planes[0], ks._planes[1]]
+        tgt += [kt._planes[0], kt._planes[1]]
+        init += [T0, T0]
+    if not src:
+        return [], []
+    res = dev.icp_batch(src, tgt, np.stack(init),
+                        _lib.icp_params(method="p2plane",
+                                        max_correspondence_distance=ICP_PARAMETERS.distance_threshold))
+    out, raw = [], []
+    for k in range(len(pairs)):
+        ra, rb = res[2 * k], res[2 * k + 1]
+        t1 = HomogeneousMatrix(ra["transformation"]).t2v(n=3)
+        t2 = HomogeneousMatrix(rb["transformation"]).t2v(n=3)
+        out.append(HomogeneousMatrix(np.array([t2[0], t2[1], t1[2]]),
+                                     Euler([t1[3], t1[4], t2[5]])))
+        raw.append((ra, rb))
+    return out, raw

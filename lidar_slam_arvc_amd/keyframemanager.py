@@ -9,9 +9,9 @@ Same constructor and methods (add_keyframes :20-24, add_keyframe :26-30, load_po
   (scan-matcher chain, loop-closure candidates).
 
 ``compute_transformation`` dispatches on ``method`` exactly like the reference: 'icppointpoint'
--> P2P, 'icppointplane' -> P2Plane; 'icp2planes' / 'fpfh' are not on the device path yet
- and raise NotImplementedError; an unknown method prints and returns None, as in the
-reference (:70-72).
+-> P2P, 'icppointplane' -> P2Plane, 'icp2planes' -> local_registration_two_planes (:66-67);
+'fpfh' is not on the device path yet and raises NotImplementedError; an
+unknown method prints and returns None, as in the reference (:70-72).
 """
 from __future__ import annotations
 
@@ -79,9 +79,12 @@ class KeyFrameManager:
         if self.method in _OPTION:
             transform = self.keyframes[i].local_registration_simple(
                 self.keyframes[j], initial_transform=Tij.array, option=_OPTION[self.method])
-        elif self.method in ("icp2planes", "fpfh"):
-            raise NotImplementedError(f"registration method {self.method!r} is not on the "
-                                      "MI355X path yet (SURVEY.md §8f)")
+        elif self.method == "icp2planes":
+            transform = self.keyframes[i].local_registration_two_planes(
+                self.keyframes[j], initial_transform=Tij.array)
+        elif self.method == "fpfh":
+            raise NotImplementedError("registration method 'fpfh' is not on the MI355X path yet "
+                                      "(SURVEY.md §8f row 4)")
         else:
             print("Unknown registration method")
             transform = None
@@ -89,6 +92,11 @@ class KeyFrameManager:
 
     def compute_transformations(self, pairs, Tijs):
         """Batched compute_transformation over independent (i, j) pairs."""
+        if self.method == "icp2planes":
+            from .keyframe import two_planes_batch
+            T, _ = two_planes_batch(self._dev, [(self.keyframes[i], self.keyframes[j])
+                                                for i, j in pairs], Tijs)
+            return T
         if self.method not in _OPTION:
             return [self.compute_transformation(i, j, T) for (i, j), T in zip(pairs, Tijs)]
         if len(pairs) == 0:

@@ -504,3 +504,147 @@ def registration_multiscale(source_raw, target_raw, init=None, scales=(0.4, 0.2,
         T = r["transformation"]
         out.append(r)
     return out
+
+
+# --------------------------------------------------------------------------------------------
+# §8f row 2, 'icp2planes': KeyFrame.calculate_plane (keyframe.py:417-437) -> [O3D]
+# PointCloud.segment_plane(distance_threshold, ransac_n=3, num_iterations), KeyFrame.segment_plane
+# (keyframe.py:439-461) and local_registration_two_planes (keyframe.py:262-295).
+# --------------------------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def _splitmix(seed, k):
+    z = (seed + (k + 1) * 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def plane_samples(seed, n, iters):
+    """Three distinct indices per RANSAC candidate from splitmix64(seed) (the build's sampler;
+    the reference's Open3D RNG is unseeded and not reproducible)."""
+    seed &= _M64
+    out = np.zeros((iters, 3), np.int64)
+    for it in range(iters):
+        u0, u1, u2 = (_splitmix(seed, 3 * it + j) for j in range(3))
+        i0 = u0 % n
+        i1 = u1 % (n - 1)
+        i1 += i1 >= i0
+        i2 = u2 % (n - 2)
+        lo, hi = min(i0, i1), max(i0, i1)
+        i2 += i2 >= lo
+        i2 += i2 >= hi
+        out[it] = (i0, i1, i2)
+    return out
+
+
+def _triangle_plane(p0, p1, p2):
+    """TriangleMesh::ComputeTrianglePlane: unit (p1 - p0) x (p2 - p0), d = -n . p0."""
+    e0, e1 = p1 - p0, p2 - p0
+    a = e0[1] * e1[2] - e0[2] * e1[1]
+    b = e0[2] * e1[0] - e0[0] * e1[2]
+    c = e0[0] * e1[1] - e0[1] * e1[0]
+    nrm = math.sqrt((a * a + b * b) + c * c)
+    if nrm == 0.0:
+        return None
+    a, b, c = a / nrm, b / nrm, c / nrm
+    return np.array([a, b, c, -((a * p0[0] + b * p0[1]) + c * p0[2])])
+
+
+def _plane_dist(pl, P):
+    return np.abs(((pl[0] * P[:, 0] + pl[1] * P[:, 1]) + pl[2] * P[:, 2]) + pl[3])
+
+
+def segment_plane_ransac(points, distance_threshold=0.01, num_iterations=1000, seed=0,
+                         probability=0.99999999):
+    """[O3D] PointCloud::SegmentPlane, sequential form: candidates scored by inlier count then
+    error / sqrt(count) (error summed in index order); stop once the evaluated count exceeds
+    log(1 - p) / log(1 - fitness^3) of the best; refit (GetPlaneFromPoints) to the winner's
+    inliers. Returns (plane[4], inlier indices)."""
+    P = np.asarray(points, dtype=np.float64)
+    n = len(P)
+    if n < 3:
+        raise RuntimeError("There must be at least 'ransac_n' points.")
+    samples = plane_samples(seed, n, num_iterations)
+    best, bfit, brmse = None, 0.0, 0.0
+    break_it, count = math.inf, 0
+    for it in range(num_iterations):
+        if count > break_it:
+            continue
+        pl = _triangle_plane(*P[samples[it]])
+        if pl is None:
+            continue
+        d = _plane_dist(pl, P)
+        m = d <= distance_threshold
+        k = int(m.sum())
+        err = float(np.cumsum(d[m])[-1]) if k else 0.0      # sequential, index order
+        fit = k / n if k else 0.0
+        rmse = err / math.sqrt(k) if k else 0.0
+        if fit > bfit or (fit == bfit and rmse < brmse):
+            best, bfit, brmse = pl, fit, rmse
+            break_it = (min(math.log(1 - probability) / math.log(1 - fit ** 3), num_iterations)
+                        if fit < 1.0 else 0.0)
+        count += 1
+    if best is None:
+        return np.zeros(4), np.zeros(0, np.int64)
+    inl = np.nonzero(_plane_dist(best, P) <= distance_threshold)[0]
+    Q = P[inl]
+    cen = Q.sum(axis=0) / len(Q)
+    r = Q - cen
+    xx, xy, xz = (r[:, 0] * r[:, 0]).sum(), (r[:, 0] * r[:, 1]).sum(), (r[:, 0] * r[:, 2]).sum()
+    yy, yz, zz = (r[:, 1] * r[:, 1]).sum(), (r[:, 1] * r[:, 2]).sum(), (r[:, 2] * r[:, 2]).sum()
+    dx, dy, dz = yy * zz - yz * yz, xx * zz - xz * xz, xx * yy - xy * xy
+    if dx > dy and dx > dz:
+        abc = np.array([dx, xz * yz - xy * zz, xy * yz - xz * yy])
+    elif dy > dz:
+        abc = np.array([xz * yz - xy * zz, dy, xy * xz - yz * xx])
+    else:
+        abc = np.array([xy * yz - xz * yy, xy * xz - yz * xx, dz])
+    nrm = math.sqrt(float(abc @ abc))
+    if nrm == 0.0:
+        return np.zeros(4), inl
+    abc = abc / nrm
+    return np.array([abc[0], abc[1], abc[2], -float(abc @ cen)]), inl
+
+
+def calculate_plane(points, height=-0.5, threshold=0.01, num_iterations=1000, seed=0):
+    """KeyFrame.calculate_plane (keyframe.py:417-437): RANSAC over the points with z < height."""
+    P = np.asarray(points, dtype=np.float64)
+    return segment_plane_ransac(P[P[:, 2] < height], threshold, num_iterations, seed)[0]
+
+
+def segment_plane(points, plane_model, threshold=0.4):
+    """KeyFrame.segment_plane (keyframe.py:439-461): (ground, non-ground) in index order."""
+    P = np.asarray(points, dtype=np.float64)
+    a, b, c, d = plane_model
+    dist = np.abs(a * P[:, 0] + b * P[:, 1] + c * P[:, 2] + d) / np.sqrt(a * a + b * b + c * c)
+    m = dist < threshold
+    return P[m], P[~m]
+
+
+def preprocess_icp2planes(points_raw, voxel_size=None, seed=0):
+    """KeyFrame.preprocess_icp2planes (keyframe.py:164-189): filter (+voxel), plane, split,
+    normals r = 0.5 on the ground part and r = 0.3 on the rest (max_nn 300 both)."""
+    P = filter_radius_height(points_raw)
+    if voxel_size is not None:
+        P = voxel_down_sample(P, voxel_size)[1]
+    plane = calculate_plane(P, seed=seed)
+    g, ng = segment_plane(P, plane)
+    return dict(plane=plane, ground=g, rest=ng, ground_normals=estimate_normals(g, 0.5, 300),
+                rest_normals=estimate_normals(ng, 0.3, 300))
+
+
+def registration_two_planes(src, tgt, init=None, max_corr=DISTANCE_THRESHOLD):
+    """local_registration_two_planes (keyframe.py:262-295): P2Plane ICP of the ground parts and
+    of the non-ground parts from the same guess; x, y, yaw from the second, z, roll, pitch from
+    the first (t2v(n=3) / Euler XYZ, artelib)."""
+    from lidar_slam_arvc_amd.se3 import Euler, HomogeneousMatrix   # host math, reference-pinned
+    ra = registration_icp(src["ground"], tgt["ground"], max_corr, init, "p2plane",
+                          tgt["ground_normals"])
+    rb = registration_icp(src["rest"], tgt["rest"], max_corr, init, "p2plane",
+                          tgt["rest_normals"])
+    t1 = HomogeneousMatrix(ra["transformation"]).t2v(n=3)
+    t2 = HomogeneousMatrix(rb["transformation"]).t2v(n=3)
+    T = HomogeneousMatrix(np.array([t2[0], t2[1], t1[2]]), Euler([t1[3], t1[4], t2[5]]))
+    return T.array, ra, rb

@@ -123,3 +123,34 @@ def test_norm_formula_matches_numpy():
     rng = np.random.default_rng(7)
     for v in rng.normal(size=(2000, 3)) * 9:
         assert O._norm1(v) == np.linalg.norm(v)
+
+
+# ------------------------------------------------------------------ icp2planes (§8f row 2)
+def test_plane_sampler_matches_library():
+    from lidar_slam_arvc_amd import _lib
+    for seed, n in [(0, 3), (1, 10), (2**63 + 5, 100000)]:
+        a = O.plane_samples(seed, n, 200)
+        assert np.array_equal(a, _lib.plane_samples(seed, n, 200))
+        assert all(len(set(r)) == 3 for r in a.tolist())
+        assert a.min() >= 0 and a.max() < n
+
+
+def test_ransac_recovers_plane():
+    rng = np.random.default_rng(3)
+    xy = rng.uniform(-10, 10, size=(3000, 2))
+    z = 0.02 * xy[:, 0] - 0.01 * xy[:, 1] - 0.7 + rng.normal(scale=0.002, size=3000)
+    P = np.column_stack([xy, z])
+    P = np.vstack([P, rng.uniform(-10, 10, size=(500, 3))])        # outliers
+    plane, inl = O.segment_plane_ransac(P, 0.01, 1000, seed=1)
+    n = np.array([-0.02, 0.01, 1.0]) / np.linalg.norm([-0.02, 0.01, 1.0])
+    s = np.sign(plane[2])
+    assert np.abs(s * plane[:3] - n).max() < 1e-3
+    assert abs(s * plane[3] - 0.7 * n[2]) < 5e-3
+    assert len(inl) >= 2800
+    g, r = O.segment_plane(P, plane, 0.4)
+    assert len(g) + len(r) == len(P) and len(g) >= 3000
+
+
+def test_ransac_too_few_points():
+    with pytest.raises(RuntimeError, match="ransac_n"):
+        O.segment_plane_ransac(np.zeros((2, 3)))
