@@ -609,16 +609,10 @@ __device__ __forceinline__ int sel_classify(const Sel &S, double d2, uint32_t k)
     return b < S.b ? -1 : (b > S.b ? 1 : 0);
 }
 
-__global__ void __launch_bounds__(PT_THREADS)
-normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
-               unsigned long long *stats) {
-    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
-    uint32_t *H = lds + threadIdx.x * HSTRIDE;
+// The normal of point j of cloud C by one lane (H: the lane's HSTRIDE-word LDS row).
+__device__ void normal_lane(const CloudDev &C, int j, const NormalParams &np,
+                            unsigned long long *stats, uint32_t *H) {
     uint8_t *H8 = reinterpret_cast<uint8_t *>(H);
-    const Seg s = segs[blockIdx.x];
-    const CloudDev C = cd[s.cloud];
-    const int j = s.start + threadIdx.x;
-    if (j >= C.n) return;
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
     float4 *nrm = const_cast<float4 *>(C.nrm);
@@ -778,6 +772,325 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
         if (rank < need) cum_add(f, make_off(lsm_ld(C.xyz, ke), qx, qy, qz));
     }
     nrm[j] = normal_from_cum(f);
+}
+
+__global__ void __launch_bounds__(PT_THREADS)
+normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
+               unsigned long long *stats) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int j = s.start + threadIdx.x;
+    if (j < C.n) normal_lane(C, j, np, stats, lds + threadIdx.x * HSTRIDE);
+}
+
+// ------------------------------------------------------------------------------------------
+// normals, split by neighbourhood size
+// ------------------------------------------------------------------------------------------
+// normals_sparse_kernel: one lane per point. The cells a ball can touch bound its size; when
+// that bound is at most dense_t (<= max_nn) the lane scans its ball once (no kNN truncation is
+// possible) and writes the normal. Larger neighbourhoods -- the near field, where balls hold
+// 300 to several thousand points -- go to a queue for normals_dense_kernel: one wave per point,
+// 64 candidates per step from contiguous (coalesced) runs, an LDS histogram per wave and the
+// same exact kNN-300 selection (Sel) as the per-lane path, with every lane of the wave sharing
+// one selection state.
+struct DenseItem {
+    int32_t cloud;
+    int32_t j;
+};
+
+__device__ __forceinline__ void cum_in_ball(Cum &c, const NormalParams &np, float4 qf, double qx,
+                                            double qy, double qz, const float4 &p) {
+    const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
+    const float f = dx * dx + dy * dy + dz * dz;
+    if (f < np.r2_lo) {
+        cum_add_pt(c, p, qx, qy, qz);
+    } else if (f <= np.r2_hi) {
+        const Off o = make_off(p, qx, qy, qz);
+        if (o.d2 < np.r2) cum_add_pt(c, p, qx, qy, qz);
+    }
+}
+
+__global__ void __launch_bounds__(PT_THREADS)
+normals_sparse_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, int dense_t,
+                      DenseItem *__restrict__ dq, uint32_t *__restrict__ dqn) {
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int j = s.start + threadIdx.x;
+    const bool live = j < C.n;
+    bool dense = false;
+    if (live) {
+        const float4 qf = lsm_ld(C.xyz, j);
+        uint32_t bound = 0;
+        ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float, float) { bound += b - a; });
+        dense = bound > uint32_t(dense_t);
+        if (!dense) {
+            const double qx = qf.x, qy = qf.y, qz = qf.z;
+            Cum c = {};
+            ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+                scan_run(C.xyz, a, b, xl, xh,
+                         [&](const float4 &p, uint32_t) { cum_in_ball(c, np, qf, qx, qy, qz, p); });
+            });
+            const_cast<float4 *>(C.nrm)[j] = normal_from_cum(c);
+        }
+    }
+    const uint64_t m = __ballot(dense);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(dqn, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, LSM_WAVE);
+    if (dense) dq[base + __popcll(m & ((uint64_t(1) << lane) - 1))] = {s.cloud, j};
+}
+
+// the per-lane normal of the queued (large-neighbourhood) points: compacted, so every lane of a
+// wave runs the kNN-truncation path
+__global__ void __launch_bounds__(PT_THREADS)
+normals_queue_kernel(const CloudDev *cd, NormalParams np, const DenseItem *__restrict__ dq,
+                     const uint32_t *__restrict__ dqn, unsigned long long *stats) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    const uint32_t total = *dqn;
+    for (uint32_t it = blockIdx.x * PT_THREADS + threadIdx.x; it < total;
+         it += gridDim.x * PT_THREADS) {
+        const DenseItem d = dq[it];
+        normal_lane(cd[d.cloud], d.j, np, stats, lds + threadIdx.x * HSTRIDE);
+    }
+}
+
+// ---- wave-cooperative helpers (every lane of the wave works on the same query point) ----
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <typename T>
+__device__ __forceinline__ T wsum(T v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, LSM_WAVE);
+    return v;
+}
+
+__device__ __forceinline__ Cum wave_cum(const Cum &c) {
+    Cum t;
+    t.sx = wsum(c.sx);
+    t.sy = wsum(c.sy);
+    t.sz = wsum(c.sz);
+    t.sxx = wsum(c.sxx);
+    t.sxy = wsum(c.sxy);
+    t.sxz = wsum(c.sxz);
+    t.syy = wsum(c.syy);
+    t.syz = wsum(c.syz);
+    t.szz = wsum(c.szz);
+    t.n = wsum(c.n);
+    return t;
+}
+
+// Every point of the runs a radius-r ball around qf touches, 64 per step: body(p, k, ok) runs on
+// every lane (ok: the lane's point is inside its run's x window). Runs are x-sorted, so a step
+// that reaches past the window ends the run.
+template <typename F>
+__device__ __forceinline__ void wave_ball_visit(const CloudDev &C, float4 qf, float r, F &&body) {
+    const int lane = threadIdx.x & 63;
+    const float *xs = reinterpret_cast<const float *>(C.xyz);
+    ball_visit_runs(C, qf, r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+        uint32_t lo = a, hi = b;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (lsm_ld(xs, size_t(mid) * 4) < xl) lo = mid + 1;
+            else hi = mid;
+        }
+        for (uint32_t base = lo; base < b; base += LSM_WAVE) {
+            const uint32_t k = base + lane;
+            const bool in = k < b;
+            const float4 p = lsm_ld(C.xyz, in ? k : b - 1);
+            body(p, k, in && p.x <= xh);
+            if (__ballot(in && p.x > xh)) break;
+        }
+    });
+}
+
+constexpr int DW = 4;        // waves (dense points in flight) per workgroup
+constexpr int NBR = 128;     // refinement bins (u32 LDS counters per wave)
+constexpr int MCAP = 64;     // final member list: one member per lane
+
+__global__ void __launch_bounds__(DW * LSM_WAVE)
+normals_dense_kernel(const CloudDev *cd, NormalParams np, const DenseItem *__restrict__ dq,
+                     const uint32_t *__restrict__ dqn, unsigned long long *stats) {
+    __shared__ uint32_t hist[DW][NBR];
+    __shared__ double md2[DW][MCAP];
+    __shared__ uint32_t mk[DW][MCAP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t *H = hist[w];
+    const uint32_t total = *dqn;
+    for (uint32_t it = blockIdx.x * DW + w; it < total; it += gridDim.x * DW) {
+        const DenseItem d = dq[it];
+        const CloudDev C = cd[d.cloud];
+        const float4 qf = lsm_ld(C.xyz, d.j);
+        const double qx = qf.x, qy = qf.y, qz = qf.z;
+        float4 *nrm = const_cast<float4 *>(C.nrm);
+        for (int b = lane; b < NBR; b += LSM_WAVE) H[b] = 0;
+        wave_sync();
+        // pass 1: count, cumulants and the level-0 histogram (128 bins of d2 over [0, r^2));
+        // f32 decisions where they are certain, the exact f64 distance otherwise (see
+        // normals_kernel)
+        Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
+        Cum c = {};
+        wave_ball_visit(C, qf, np.r, [&](const float4 &p, uint32_t k, bool ok) {
+            if (!ok) return;
+            const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
+            const float f = dx * dx + dy * dy + dz * dz;
+            const float t = f * np.hscale;
+            const float fr = t - floorf(t);
+            int bb = -1;
+            if (f < np.r2_lo && fr > 2e-4f && fr < 1.f - 2e-4f) {
+                bb = int(t);
+            } else if (f <= np.r2_hi) {
+                const Off o = make_off(p, qx, qy, qz);
+                if (o.d2 < np.r2) bb = sel_level_bin(S, o.d2, k);
+            }
+            if (bb >= 0) {
+                cum_add_pt(c, p, qx, qy, qz);
+                atomicAdd(&H[bb], 1u);
+            }
+        });
+        const int count = wsum(c.n);
+        if (count <= np.max_nn) {
+            const Cum t = wave_cum(c);
+            if (lane == 0) nrm[d.j] = normal_from_cum(t);
+            continue;
+        }
+        if (stats && lane == 0) atomicAdd(stats, 1ull);
+        double top = np.r2;
+        uint32_t need = uint32_t(np.max_nn);
+        for (int lev = 0; lev < MAX_REFINE; ++lev) {
+            wave_sync();
+            // first bin whose running count reaches `need`: two bins per lane, wave scan
+            const int nb = S.nb;
+            const int b0 = 2 * lane, b1 = 2 * lane + 1;
+            const uint32_t h0 = b0 < nb ? H[b0] : 0u, h1 = b1 < nb ? H[b1] : 0u;
+            uint32_t incl = h0 + h1;
+#pragma unroll
+            for (int off = 1; off < LSM_WAVE; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off, LSM_WAVE);
+                if (lane >= off) incl += y;
+            }
+            const uint32_t excl = incl - h0 - h1;
+            // this lane's bin reaching `need` first (at most one lane's first crossing)
+            int mine = -1;
+            uint32_t acc_l = 0;
+            if (b0 < nb && excl + h0 >= need && excl < need) {
+                mine = b0;
+                acc_l = excl;
+            } else if (b1 < nb && excl + h0 + h1 >= need && excl + h0 < need) {
+                mine = b1;
+                acc_l = excl + h0;
+            }
+            const uint64_t hit = __ballot(mine >= 0);
+            int bstar = nb - 1;
+            uint32_t acc = 0;
+            if (hit) {
+                const int src = __ffsll((unsigned long long)hit) - 1;
+                bstar = __shfl(mine, src, LSM_WAVE);
+                acc = __shfl(acc_l, src, LSM_WAVE);
+            } else {   // fewer than `need` in total: take everything (cannot happen: count > max_nn)
+                acc = __shfl(incl, LSM_WAVE - 1, LSM_WAVE) - H[nb - 1];
+            }
+            const uint32_t bin_count = H[bstar];
+            need -= acc;
+            S.b = bstar;
+            if (!S.by_idx) top = fmin(top, S.lo + double(bstar + 1) / S.scale);
+            if (bin_count <= uint32_t(MCAP)) break;
+            // next level over the chosen bin's range, clipped to the members' exact extremes
+            Sel next = S;
+            {
+                const double vlo = S.by_idx ? double(S.klo) : S.dlo;
+                const double vhi = S.by_idx ? double(S.khi) + 1.0 : S.dhi;
+                const double elo = fmax(S.lo + double(bstar) / S.scale, vlo);
+                const double ehi = fmin(S.lo + double(bstar + 1) / S.scale, vhi);
+                next.lo = elo;
+                next.scale = ehi > elo ? double(NBR) / (ehi - elo) : S.scale * double(NBR);
+                next.nb = NBR;
+            }
+            double dmin, dmax;
+            uint32_t kmin, kmax;
+            auto refine = [&](const Sel &lv) {
+                wave_sync();
+                for (int b = lane; b < NBR; b += LSM_WAVE) H[b] = 0;
+                wave_sync();
+                double lmin = INFINITY, lmax = -INFINITY;
+                uint32_t kl = 0xffffffffu, kh = 0u;
+                wave_ball_visit(C, qf, sel_radius(top, np.r), [&](const float4 &p, uint32_t k, bool ok) {
+                    Off o;
+                    if (ok && in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
+                        atomicAdd(&H[sel_level_bin(lv, o.d2, k)], 1u);
+                        lmin = fmin(lmin, o.d2);
+                        lmax = fmax(lmax, o.d2);
+                        kl = min(kl, k);
+                        kh = max(kh, k);
+                    }
+                });
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) {
+                    lmin = fmin(lmin, __shfl_xor(lmin, off, LSM_WAVE));
+                    lmax = fmax(lmax, __shfl_xor(lmax, off, LSM_WAVE));
+                    kl = min(kl, (uint32_t)__shfl_xor((int)kl, off, LSM_WAVE));
+                    kh = max(kh, (uint32_t)__shfl_xor((int)kh, off, LSM_WAVE));
+                }
+                dmin = lmin;
+                dmax = lmax;
+                kmin = kl;
+                kmax = kh;
+            };
+            refine(next);
+            if (!S.by_idx && dmin == dmax) {
+                // every member has the same d2: order them by index instead
+                next.by_idx = 1;
+                next.lo = double(kmin);
+                next.scale = double(NBR) / (double(kmax - kmin) + 1.0);
+                refine(next);
+            }
+            next.dlo = dmin;
+            next.dhi = dmax;
+            next.klo = next.by_idx ? kmin : 0u;
+            next.khi = next.by_idx ? kmax : 0xffffffffu;
+            top = fmin(top, dmax);
+            S = next;
+        }
+        // final pass: everything below, plus the `need` smallest members by (d2, k)
+        wave_sync();
+        Cum f = {};
+        uint32_t m = 0;
+        wave_ball_visit(C, qf, sel_radius(top, np.r), [&](const float4 &p, uint32_t k, bool ok) {
+            Off o;
+            const bool in = ok && in_ball(np, qf, qx, qy, qz, p, o);
+            const int cl = in ? sel_classify(S, o.d2, k) : 1;
+            if (cl < 0) cum_add_pt(f, p, qx, qy, qz);
+            const uint64_t mm = __ballot(cl == 0);
+            if (cl == 0) {
+                const uint32_t slot = m + __popcll(mm & ((uint64_t(1) << lane) - 1));
+                if (slot < uint32_t(MCAP)) {
+                    md2[w][slot] = o.d2;
+                    mk[w][slot] = k;
+                }
+            }
+            m += __popcll(mm);
+        });
+        wave_sync();
+        const uint32_t M = m < uint32_t(MCAP) ? m : uint32_t(MCAP);
+        if (uint32_t(lane) < M) {
+            const double de = md2[w][lane];
+            const uint32_t ke = mk[w][lane];
+            uint32_t rank = 0;
+            for (uint32_t g = 0; g < M; ++g) {
+                const double dg = md2[w][g];
+                rank += (dg < de || (dg == de && mk[w][g] < ke)) ? 1u : 0u;
+            }
+            if (rank < need) cum_add_pt(f, lsm_ld(C.xyz, ke), qx, qy, qz);
+        }
+        const Cum t = wave_cum(f);
+        if (lane == 0) nrm[d.j] = normal_from_cum(t);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1242,7 +1555,36 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 d_ns = (unsigned long long *)ctx->buf("n_stats", 8 * 8);
                 LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 64, st));
             }
-            normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
+            static const bool legacy = getenv("LSM_NORMALS_LEGACY") != nullptr;
+            static const int dense_env = [] {
+                const char *e = getenv("LSM_NORMALS_DENSE_T");
+                return e ? atoi(e) : 128;
+            }();
+            if (legacy) {
+                normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
+            } else {
+                const int dense_t = std::max(0, std::min(dense_env, np.max_nn));
+                int64_t total_pts = 0;
+                for (uint32_t v : wn) total_pts += v;
+                DenseItem *d_dq = (DenseItem *)ctx->buf(
+                    "n_dq", size_t(std::max<int64_t>(total_pts, 1)) * sizeof(DenseItem));
+                uint32_t *d_dqn = (uint32_t *)ctx->buf("n_dqn", 4);
+                if (!d_dq || !d_dqn) return LSM_ENOMEM;
+                LSM_HIP_TRY(ctx, hipMemsetAsync(d_dqn, 0, 4, st));
+                normals_sparse_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np,
+                                                                              dense_t, d_dq, d_dqn);
+                static const bool wave_dense = getenv("LSM_NORMALS_WAVE") != nullptr;
+                if (wave_dense) {
+                    const int dgrid = std::max(1, ctx->num_cus * 8);
+                    normals_dense_kernel<<<dgrid, DW * LSM_WAVE, 0, st>>>(d_cd, np, d_dq, d_dqn,
+                                                                         d_ns);
+                } else {
+                    const int qgrid = int(std::max<int64_t>(1, std::min<int64_t>(
+                        (total_pts + PT_THREADS - 1) / PT_THREADS, int64_t(ctx->num_cus) * 16)));
+                    normals_queue_kernel<<<qgrid, PT_THREADS, 0, st>>>(d_cd, np, d_dq, d_dqn,
+                                                                       d_ns);
+                }
+            }
             if (nstats) {
                 unsigned long long h = 0;
                 LSM_HIP_TRY(ctx, hipMemcpyAsync(&h, d_ns, 8, hipMemcpyDeviceToHost, st));

@@ -160,7 +160,9 @@ def raycast(scene: Scene, pose: np.ndarray, model: LidarModel, rng: np.random.Ge
     """Ray-cast one spinning scan; returns float32 M x 3 sensor-frame points (misses removed)."""
     d_s = model.directions()
     R, o = pose[:3, :3], pose[:3, 3]
-    d_w = d_s @ R.T
+    # d_s R^T without BLAS: this runs in worker threads, and concurrent OpenBLAS calls gave
+    # run-to-run different scans on many-core hosts
+    d_w = d_s[:, 0:1] * R[:, 0] + d_s[:, 1:2] * R[:, 1] + d_s[:, 2:3] * R[:, 2]
     near = model.max_range + 3.0
     bx = scene.boxes
     if len(bx):
@@ -284,9 +286,13 @@ def _parallel_map(fn, items):
     """Thread pool map (NumPy releases the GIL in the ray-box kernels); order-preserving."""
     from concurrent.futures import ThreadPoolExecutor
     import os
+    from threadpoolctl import threadpool_limits
     items = list(items)
     workers = max(1, min(8, os.cpu_count() or 1, len(items)))
-    if workers == 1:
-        return [fn(i) for i in items]
-    with ThreadPoolExecutor(workers) as ex:
-        return list(ex.map(fn, items))
+    # single-threaded BLAS inside the workers: the small matrix products of the pose math must
+    # not race on OpenBLAS's shared buffers (that made scans differ between runs)
+    with threadpool_limits(limits=1, user_api="blas"):
+        if workers == 1:
+            return [fn(i) for i in items]
+        with ThreadPoolExecutor(workers) as ex:
+            return list(ex.map(fn, items))
