@@ -1555,7 +1555,12 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 d_ns = (unsigned long long *)ctx->buf("n_stats", 8 * 8);
                 LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 64, st));
             }
-            static const bool legacy = getenv("LSM_NORMALS_LEGACY") != nullptr;
+            // default: one lane per point in place (cell-sorted order keeps a wave's points
+            // together). LSM_NORMALS_SPLIT=1: sparse kernel + queue of the large
+            // neighbourhoods (per lane, or one wave per point with LSM_NORMALS_WAVE=1) --
+            // measured slower, kept for experiments.
+            static const bool legacy = getenv("LSM_NORMALS_SPLIT") == nullptr &&
+                                       getenv("LSM_NORMALS_WAVE") == nullptr;
             static const int dense_env = [] {
                 const char *e = getenv("LSM_NORMALS_DENSE_T");
                 return e ? atoi(e) : 128;
