@@ -36,10 +36,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="hdl64_seq", choices=["hdl64_seq", "ouster_multiscale"],
+    ap.add_argument("--workload", default="hdl64_seq",
+                    choices=["hdl64_seq", "ouster_multiscale", "loop_closure"],
                     help="hdl64_seq: C2/C3 64k HDL-64 sequence pairs (the headline line); "
-                         "ouster_multiscale: C5 256k Ouster-128, voxel 0.4/0.2/0.1 m chain")
-    ap.add_argument("--pairs-per-gpu", type=int, default=0, help="0: 256 (hdl64), 32 (ouster)")
+                         "ouster_multiscale: C5 256k Ouster-128, voxel 0.4/0.2/0.1 m chain; "
+                         "loop_closure: C4 independent 64k revisit pairs (sharded, no halo)")
+    ap.add_argument("--pairs-per-gpu", type=int, default=0,
+                    help="0: 256 (hdl64), 32 (ouster), 512 (loop_closure)")
     ap.add_argument("--seed", type=int, default=-1, help="-1: 3 (hdl64), 5 (ouster)")
     ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
     ap.add_argument("--cpu-sample-pairs", type=int, default=2)
@@ -84,6 +87,26 @@ def cpu_baseline_multiscale(seq, n_pairs: int, method: str, threads: int):
                       f"{dt:.1f} s"}
 
 
+def cpu_baseline_pairs(seq, P: int, n_pairs: int, method: str, threads: int):
+    """The f64 oracle on the first n_pairs independent revisit pairs (both clouds pre-processed)."""
+    from oracle import open3d_restated as O
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    O.WORKERS = threads
+    t0 = time.perf_counter()
+    for k in range(n_pairs):
+        tgt = O.filter_radius_height(seq.scans[k])
+        src = O.filter_radius_height(seq.scans[P + k])
+        nrm = O.estimate_normals(tgt) if method == "p2plane" else None
+        O.filter_radius_height(seq.scans[P + k])
+        if method == "p2plane":
+            O.estimate_normals(src)      # the reference pre-processes both keyframes
+        O.registration_icp(src, tgt, 10.0, seq.priors[k], method, nrm)
+    dt = time.perf_counter() - t0
+    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n_pairs} revisit pairs (both keyframes pre-processed per pair), f64 "
+                      f"NumPy/SciPy cKDTree oracle, {dt:.1f} s"}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -102,12 +125,19 @@ def main():
     from lidar_slam_arvc_amd.distributed import compose_global_sharded
 
     ouster = args.workload == "ouster_multiscale"
-    P = args.pairs_per_gpu or (32 if ouster else 256)
+    loop = args.workload == "loop_closure"
+    P = args.pairs_per_gpu or (32 if ouster else (512 if loop else 256))
     first = rank * P
     model = synthetic.OUSTER128 if ouster else synthetic.HDL64
-    seed = args.seed if args.seed >= 0 else (5 if ouster else 3)
-    seq = synthetic.make_sequence(P + 1, seed=seed, model=model, first_index=first)
+    seed = args.seed if args.seed >= 0 else (5 if ouster else (4 if loop else 3))
     dev = _lib.device(local)
+    if loop:
+        # C4: every rank owns P independent revisit pairs (its own targets and sources)
+        ps = synthetic.make_revisit_pairs(P, seed=seed, model=model, first_index=first)
+        seq = synthetic.Sequence(ps.targets + ps.sources, np.zeros((0, 4, 4)), ps.init)
+        del ps
+    else:
+        seq = synthetic.make_sequence(P + 1, seed=seed, model=model, first_index=first)
     ids = [dev.upload(s) for s in seq.scans]        # raw scans resident in HBM
     want_normals = args.method == "p2plane"
     cuda = torch.device("cuda", local)
@@ -124,6 +154,18 @@ def main():
             rel = np.stack([r["transformation"] for r in res])
             compose_global_sharded(rel, group=group, device=cuda)
             n = [dev.info(h)[1] for h in ms.handles[-1]]
+            return n, res
+    elif loop:
+        prep = _lib.prep_params(want_normals=want_normals, grid_cell=args.grid_cell)
+        icp = _lib.icp_params(method=args.method)
+
+        def step():
+            n = dev.preprocess(ids, prep)
+            res = dev.icp_batch(ids[P:], ids[:P], seq.priors, icp)
+            rel = np.stack([r["transformation"] for r in res])
+            if group is not None:   # the sequence-level exchange: gather every pair's result
+                allr = [torch.empty(P, 16, dtype=torch.float64, device=cuda) for _ in range(world)]
+                dist.all_gather(allr, torch.from_numpy(rel.reshape(P, 16)).to(cuda))
             return n, res
     else:
         prep = _lib.prep_params(want_normals=want_normals, grid_cell=args.grid_cell)
@@ -180,9 +222,14 @@ def main():
                                            for k in ("nn", "nn_fallback")}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = (cpu_baseline_multiscale(seq, max(1, args.cpu_sample_pairs // 2), args.method,
-                                           args.cpu_threads) if ouster else
-                   cpu_baseline(seq, args.cpu_sample_pairs, args.method, args.cpu_threads))
+            if ouster:
+                cpu = cpu_baseline_multiscale(seq, max(1, args.cpu_sample_pairs // 2),
+                                              args.method, args.cpu_threads)
+            elif loop:
+                cpu = cpu_baseline_pairs(seq, P, args.cpu_sample_pairs, args.method,
+                                         args.cpu_threads)
+            else:
+                cpu = cpu_baseline(seq, args.cpu_sample_pairs, args.method, args.cpu_threads)
         ms_step = dt / args.steps * 1e3
         out = {
             "metric": ("ICP keyframe-pair registrations/sec (256k-ray Ouster-128, multi-scale)"
@@ -207,6 +254,14 @@ def main():
                         "max_correspondence_distance": [2.0, 1.0, 0.5],
                         "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"}
                        if ouster else
+                       {"workload": f"hdl64_64k_{args.method}_loop_closure_pairs",
+                        "pairs_per_gpu": P, "global_pairs": world * P,
+                        "points_per_scan_post_filter": int(np.mean(n_pts)),
+                        "rays_per_scan": 65536, "method": args.method,
+                        "init": "GT (+) N(0.3 m, 3 deg yaw)",
+                        "max_correspondence_distance": 10.0,
+                        "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"}
+                       if loop else
                        {"workload": f"hdl64_64k_{args.method}_seq",
                         "pairs_per_gpu": P, "global_pairs": world * P,
                         "points_per_scan_post_filter": int(np.mean(n_pts)),
