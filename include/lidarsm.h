@@ -147,6 +147,27 @@ int lsm_plane_samples_get(uint64_t seed, int64_t n, int64_t num_iterations, int3
 int lsm_split_plane(lsm_ctx *ctx, lsm_cloud cloud, const double plane[4], double threshold,
                     lsm_cloud *ground, lsm_cloud *rest);
 
+/* 'fpfh' global registration ----------------------------------------
+ * compute_fpfh_feature(cloud, KDTreeSearchParamHybrid(radius, max_nn)) (keyframe.py:226-229):
+ * FPFH of a pre-processed cloud with normals, kept on the device; `features` (nullable) receives
+ * them, n x 33 f64 in reference order. */
+int lsm_fpfh(lsm_ctx *ctx, lsm_cloud cloud, double radius, int32_t max_nn, double *features,
+             int64_t cap);
+/* The feature matches of registration_ransac_based_on_feature_matching (keyframe.py:318-327):
+ * every source feature's exact nearest target feature; with `mutual`, only the mutual pairs
+ * unless fewer than 3 * ransac_n remain. corres: (source, target) index pairs (reference order),
+ * *n = count. */
+int lsm_feature_correspondences(lsm_ctx *ctx, lsm_cloud src, lsm_cloud tgt, int32_t mutual,
+                                int32_t ransac_n, int32_t *corres, int64_t cap, int64_t *n);
+/* RANSAC over the matches (ransac_n = 3, P2P without scaling, edge-length and distance
+ * checkers, RANSACConvergenceCriteria(max_iteration, confidence)), sequential form with
+ * splitmix64(seed) samples: the best transformation by (fitness, inlier_rmse) of one
+ * correspondence pass within max_correspondence_distance; *evaluated = hypotheses scored. */
+int lsm_ransac_feature(lsm_ctx *ctx, lsm_cloud src, lsm_cloud tgt, const int32_t *corres,
+                       int64_t n, double max_correspondence_distance, double edge_similarity,
+                       int64_t max_iteration, double confidence, uint64_t seed, double T[16],
+                       double *fitness, double *inlier_rmse, int64_t *evaluated);
+
 /* Loop-closure candidate matching (graphslam/loopclosing.py:102-144, :202-268) -------------
  * positions: m x 3 float64 trajectory (store_positions :202-211, last row = current pose).
  * index_backwards: find_index_backwards :223-237 (-1 for None).

@@ -26,6 +26,7 @@ EXPORTED = [
     "lsm_cloud_voxel_keys", "lsm_icp", "lsm_icp_batch", "lsm_icp_last_correspondences",
     "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
     "lsm_reset_stats", "lsm_ground_plane", "lsm_plane_samples_get", "lsm_split_plane",
+    "lsm_fpfh", "lsm_feature_correspondences", "lsm_ransac_feature",
 ]
 
 
@@ -92,6 +93,12 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                        C.c_uint64, C.c_double, _f64p, _i64p, _i64p]),
         "lsm_plane_samples_get": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, _i32p]),
         "lsm_split_plane": (C.c_int, [_P, C.c_int64, _f64p, C.c_double, _i64p, _i64p]),
+        "lsm_fpfh": (C.c_int, [_P, C.c_int64, C.c_double, C.c_int32, _f64p, C.c_int64]),
+        "lsm_feature_correspondences": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int32, C.c_int32,
+                                                  _i32p, C.c_int64, _i64p]),
+        "lsm_ransac_feature": (C.c_int, [_P, C.c_int64, C.c_int64, _i32p, C.c_int64, C.c_double,
+                                         C.c_double, C.c_int64, C.c_double, C.c_uint64, _f64p,
+                                         _f64p, _f64p, _i64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -198,6 +205,41 @@ class Device:
                                             float(threshold), C.byref(g), C.byref(r)),
                    "lsm_split_plane")
         return g.value, r.value
+
+    def fpfh(self, cloud: int, radius=0.3, max_nn=100, download=True):
+        """compute_fpfh_feature on the device; returns the n x 33 features (reference order)."""
+        n = self.info(cloud)[1]
+        out = np.zeros((n, 33)) if download else None
+        self.check(self.lib.lsm_fpfh(self.handle, int(cloud), float(radius), int(max_nn),
+                                     _ptr(out, C.c_double) if download else None, n),
+                   "compute_fpfh_feature")
+        return out
+
+    def feature_correspondences(self, src: int, tgt: int, mutual=True, ransac_n=3):
+        n_src = self.info(src)[1]
+        out = np.zeros((max(n_src, 1), 2), dtype=np.int32)
+        n = C.c_int64()
+        self.check(self.lib.lsm_feature_correspondences(self.handle, int(src), int(tgt),
+                                                        1 if mutual else 0, int(ransac_n),
+                                                        _ptr(out, C.c_int32), len(out),
+                                                        C.byref(n)), "feature matching")
+        return out[:n.value].copy()
+
+    def ransac_feature(self, src: int, tgt: int, corres, max_correspondence_distance=5.0,
+                       edge=0.9, max_iteration=100000, confidence=0.999, seed=0):
+        c = np.ascontiguousarray(corres, dtype=np.int32).reshape(-1, 2)
+        T = np.zeros(16)
+        fit, rmse = C.c_double(), C.c_double()
+        ev = C.c_int64()
+        self.check(self.lib.lsm_ransac_feature(self.handle, int(src), int(tgt),
+                                               _ptr(c, C.c_int32), len(c),
+                                               float(max_correspondence_distance), float(edge),
+                                               int(max_iteration), float(confidence),
+                                               int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(T, C.c_double),
+                                               C.byref(fit), C.byref(rmse), C.byref(ev)),
+                   "registration_ransac_based_on_feature_matching")
+        return dict(transformation=T.reshape(4, 4), fitness=fit.value, inlier_rmse=rmse.value,
+                    evaluated=ev.value)
 
     def release(self, cloud: int):
         self.check(self.lib.lsm_cloud_release(self.handle, int(cloud)), "lsm_cloud_release")

@@ -102,6 +102,8 @@ static void free_cloud(Cloud *c) {
     (void)hipFree(c->d_cell);
     (void)hipFree(c->d_vox);
     (void)hipFree(c->d_vkeys);
+    (void)hipFree(c->d_prior_ref);
+    (void)hipFree(c->d_fpfh);
     delete c;
 }
 
@@ -301,6 +303,78 @@ int lsm_split_plane(lsm_ctx *ctx, lsm_cloud cloud, const double plane[4], double
     *ground = ig;
     *rest = ir;
     return LSM_OK;
+}
+
+int lsm_fpfh(lsm_ctx *ctx, lsm_cloud cloud, double radius, int32_t max_nn, double *features,
+             int64_t cap) {
+    if (!ctx) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!c->processed || !c->has_normals) {
+        ctx->set_error("ComputeFPFHFeature needs a cloud with normals (pre-process with normals)");
+        return LSM_ESTATE;
+    }
+    if (!(radius > 0) || max_nn < 1) {
+        ctx->set_error("Invalid KDTreeSearchParamHybrid (radius <= 0 or max_nn < 1)");
+        return LSM_EINVAL;
+    }
+    (void)hipSetDevice(ctx->device);
+    int rc = lsm_fpfh_run(ctx, c, radius, max_nn);
+    if (rc) return rc;
+    if (features && c->n > 0) {
+        LSM_HIP_TRY(ctx, hipMemcpy(features, c->d_fpfh, size_t(std::min<int64_t>(cap, c->n)) * 33 * 8,
+                                   hipMemcpyDeviceToHost));
+    }
+    return LSM_OK;
+}
+
+int lsm_feature_correspondences(lsm_ctx *ctx, lsm_cloud src, lsm_cloud tgt, int32_t mutual,
+                                int32_t ransac_n, int32_t *corres, int64_t cap, int64_t *n) {
+    if (!ctx || !n) return LSM_EINVAL;
+    Cloud *s = find_cloud(ctx, src), *t = find_cloud(ctx, tgt);
+    if (!s || !t) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!s->d_fpfh || !t->d_fpfh || s->fpfh_n != s->n || t->fpfh_n != t->n) {
+        ctx->set_error("compute the FPFH features of both clouds first (lsm_fpfh)");
+        return LSM_ESTATE;
+    }
+    (void)hipSetDevice(ctx->device);
+    return lsm_feature_corr_run(ctx, s, t, mutual, ransac_n, corres, cap, n);
+}
+
+int lsm_ransac_feature(lsm_ctx *ctx, lsm_cloud src, lsm_cloud tgt, const int32_t *corres,
+                       int64_t n, double max_correspondence_distance, double edge_similarity,
+                       int64_t max_iteration, double confidence, uint64_t seed, double T[16],
+                       double *fitness, double *inlier_rmse, int64_t *evaluated) {
+    if (!ctx || !T || !fitness || !inlier_rmse || !evaluated || (n > 0 && !corres)) return LSM_EINVAL;
+    Cloud *s = find_cloud(ctx, src), *t = find_cloud(ctx, tgt);
+    if (!s || !t) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!s->processed || !t->processed) {
+        ctx->set_error("clouds not pre-processed");
+        return LSM_ESTATE;
+    }
+    if (!(max_correspondence_distance > 0) || max_iteration < 0 || max_iteration > (int64_t(1) << 24) ||
+        !(confidence > 0 && confidence < 1)) {
+        ctx->set_error("invalid RANSAC parameters");
+        return LSM_EINVAL;
+    }
+    for (int64_t k = 0; k < n; ++k)
+        if (corres[2 * k] < 0 || corres[2 * k] >= s->n || corres[2 * k + 1] < 0 ||
+            corres[2 * k + 1] >= t->n) {
+            ctx->set_error("correspondence index out of range");
+            return LSM_EINVAL;
+        }
+    (void)hipSetDevice(ctx->device);
+    return lsm_ransac_run(ctx, s, t, corres, n, max_correspondence_distance, edge_similarity,
+                          max_iteration, confidence, seed, T, fitness, inlier_rmse, evaluated);
 }
 
 int lsm_cloud_release(lsm_ctx *ctx, lsm_cloud cloud) {

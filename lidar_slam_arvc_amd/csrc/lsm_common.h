@@ -29,6 +29,8 @@ struct CloudDev {
     int nx, ny, nz;             // cells per axis
     int nbx, nby, nbz;          // 4x4x4 blocks per axis
     int n;
+    const uint32_t *perm;       // sorted position -> reference order
+    const float4 *prior_ref;    // prior normals in reference order (orientation), or nullptr
 };
 
 #define LSM_BLK 4          // cells per block edge

@@ -29,6 +29,10 @@ struct Cloud {
     double *d_vox = nullptr;      // voxel centroids (f64, voxel-key order), voxelised clouds only
     int32_t *d_vkeys = nullptr;   // voxel keys (int32 x 3)
     int64_t vox_cap = 0;
+    double *d_fpfh = nullptr;     // FPFH features, n x 33, reference order
+    int64_t fpfh_cap = 0, fpfh_n = 0;
+    float4 *d_prior_ref = nullptr; // prior normals (reference order) of a split cloud
+    int64_t prior_n = 0;
     bool processed = false;
     bool has_normals = false;
     bool voxelized = false;
@@ -101,3 +105,9 @@ int lsm_ground_plane_run(lsm_ctx *ctx, Cloud *c, double height, double thr, int6
 int lsm_split_plane_run(lsm_ctx *ctx, Cloud *c, const double plane[4], double thr, Cloud *g,
                         Cloud *r);
 void lsm_plane_samples(uint64_t seed, int64_t n, int64_t iters, int32_t *out);
+int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn);
+int lsm_feature_corr_run(lsm_ctx *ctx, Cloud *s, Cloud *t, int mutual, int ransac_n,
+                         int32_t *out, int64_t cap, int64_t *n_out);
+int lsm_ransac_run(lsm_ctx *ctx, Cloud *src, Cloud *tgt, const int32_t *corr, int64_t ncorr,
+                   double max_corr, double edge, int64_t iters, double confidence, uint64_t seed,
+                   double T[16], double *fitness, double *rmse, int64_t *evaluated);

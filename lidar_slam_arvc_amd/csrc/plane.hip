@@ -20,9 +20,11 @@
 
 #include <cmath>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #include "lsm_ctx.h"
+#include "lsm_umeyama.h"
 
 namespace {
 
@@ -70,6 +72,13 @@ __device__ __forceinline__ double dot4(const double *pl, double x, double y, dou
     // ((a x + b y) + c z) + d, every product and sum rounded (no contraction)
     return lsm_dadd(lsm_dadd(lsm_dadd(lsm_dmul(pl[0], x), lsm_dmul(pl[1], y)),
                              lsm_dmul(pl[2], z)), pl[3]);
+}
+
+// sorted normals -> reference order
+__global__ void ref_normals_kernel(const float4 *__restrict__ nrm, const uint32_t *__restrict__ perm,
+                                   int n, float4 *__restrict__ out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) out[perm[j]] = nrm[j];
 }
 
 // z < height subset of the reference-order points, in order
@@ -257,8 +266,10 @@ ransac_finish_kernel(const double *__restrict__ sub, int n_sub, const double *__
 
 // segment_plane: |a x + b y + c z + d| / sqrt(a a + b b + c c) < thr (numpy's evaluation order)
 __global__ void __launch_bounds__(CT)
-split_kernel(const double *__restrict__ P, int n, const double *__restrict__ plane, double thr,
-             float *__restrict__ ground, float *__restrict__ rest, uint32_t *__restrict__ counts) {
+split_kernel(const double *__restrict__ P, const float4 *__restrict__ N, int n,
+             const double *__restrict__ plane, double thr, float *__restrict__ ground,
+             float *__restrict__ rest, float4 *__restrict__ gN, float4 *__restrict__ rN,
+             uint32_t *__restrict__ counts) {
     const double a = plane[0], b = plane[1], c = plane[2], d = plane[3];
     const double den = sqrt(lsm_dadd(lsm_dadd(lsm_dmul(a, a), lsm_dmul(b, b)), lsm_dmul(c, c)));
     uint32_t tg = 0, tr = 0;
@@ -274,6 +285,7 @@ split_kernel(const double *__restrict__ P, int n, const double *__restrict__ pla
             ground[3 * slot] = float(P[3 * i]);
             ground[3 * slot + 1] = float(P[3 * i + 1]);
             ground[3 * slot + 2] = float(P[3 * i + 2]);
+            if (N) gN[slot] = N[i];
         },
         tg);
     compact_block(
@@ -282,11 +294,83 @@ split_kernel(const double *__restrict__ P, int n, const double *__restrict__ pla
             rest[3 * slot] = float(P[3 * i]);
             rest[3 * slot + 1] = float(P[3 * i + 1]);
             rest[3 * slot + 2] = float(P[3 * i + 2]);
+            if (N) rN[slot] = N[i];
         },
         tr);
     if (threadIdx.x == 0) {
         counts[0] = tg;
         counts[1] = tr;
+    }
+}
+
+// Feature-RANSAC hypotheses (RegistrationRANSACBasedOnCorrespondence, ransac_n = 3): one lane
+// per iteration -- the sampled correspondences' Umeyama transform, the edge-length (similarity)
+// and distance checkers, and the correspondence inlier ratio (|T s - t|^2 < max_corr^2 over all
+// correspondences) that drives the early exit.
+__global__ void __launch_bounds__(LSM_WAVE)
+ransac_hyp_kernel(const double *__restrict__ S, const double *__restrict__ Tg,
+                  const int32_t *__restrict__ corr, int ncorr, const int32_t *__restrict__ samples,
+                  int iters, double max_corr, double edge, double *__restrict__ T,
+                  int32_t *__restrict__ valid, double *__restrict__ ratio) {
+    const int it = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = it < iters;
+    double D[16];
+    double ps[3][3], pt[3][3];
+    if (ok) {
+        for (int r = 0; r < 3; ++r) {
+            const int c = samples[3 * it + r];
+            const int i = corr[2 * c], j = corr[2 * c + 1];
+            for (int d = 0; d < 3; ++d) {
+                ps[r][d] = S[3 * i + d];
+                pt[r][d] = Tg[3 * j + d];
+            }
+        }
+        double tot[32];
+        for (int k = 0; k < 32; ++k) tot[k] = 0.0;
+        for (int r = 0; r < 3; ++r) {
+            for (int d = 0; d < 3; ++d) {
+                tot[d] += ps[r][d];
+                tot[3 + d] += pt[r][d];
+            }
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) tot[6 + 3 * a + b] += pt[r][a] * ps[r][b];
+        }
+        tot[29] = 3.0;
+        lsm::umeyama_update(tot, D);
+        for (int i = 0; i < 3 && ok; ++i)
+            for (int j = i + 1; j < 3; ++j) {
+                const double ex = ps[i][0] - ps[j][0], ey = ps[i][1] - ps[j][1], ez = ps[i][2] - ps[j][2];
+                const double fx = pt[i][0] - pt[j][0], fy = pt[i][1] - pt[j][1], fz = pt[i][2] - pt[j][2];
+                const double ds = sqrt((ex * ex + ey * ey) + ez * ez);
+                const double dt = sqrt((fx * fx + fy * fy) + fz * fz);
+                if (ds < dt * edge || dt < ds * edge) ok = false;
+            }
+        for (int r = 0; r < 3 && ok; ++r) {
+            const double x = D[0] * ps[r][0] + D[1] * ps[r][1] + D[2] * ps[r][2] + D[3];
+            const double y = D[4] * ps[r][0] + D[5] * ps[r][1] + D[6] * ps[r][2] + D[7];
+            const double z = D[8] * ps[r][0] + D[9] * ps[r][1] + D[10] * ps[r][2] + D[11];
+            const double ex = pt[r][0] - x, ey = pt[r][1] - y, ez = pt[r][2] - z;
+            if (sqrt((ex * ex + ey * ey) + ez * ez) > max_corr) ok = false;
+        }
+    }
+    uint32_t in = 0;
+    if (__ballot(ok)) {
+        const double m2 = max_corr * max_corr;
+        for (int c = 0; c < ncorr; ++c) {   // every lane reads the same correspondence
+            const int i = corr[2 * c], j = corr[2 * c + 1];
+            if (!ok) continue;
+            const double sx = S[3 * i], sy = S[3 * i + 1], sz = S[3 * i + 2];
+            const double x = D[0] * sx + D[1] * sy + D[2] * sz + D[3];
+            const double y = D[4] * sx + D[5] * sy + D[6] * sz + D[7];
+            const double z = D[8] * sx + D[9] * sy + D[10] * sz + D[11];
+            const double ex = x - Tg[3 * j], ey = y - Tg[3 * j + 1], ez = z - Tg[3 * j + 2];
+            in += ((ex * ex + ey * ey) + ez * ez) < m2 ? 1u : 0u;
+        }
+    }
+    if (it < iters) {
+        for (int k = 0; k < 16; ++k) T[16 * size_t(it) + k] = ok ? D[k] : 0.0;
+        valid[it] = ok ? 1 : 0;
+        ratio[it] = ok ? double(in) / double(ncorr) : 0.0;
     }
 }
 
@@ -392,18 +476,127 @@ int lsm_split_plane_run(lsm_ctx *ctx, Cloud *c, const double plane[4], double th
     double *d_pl = (double *)ctx->buf("pl_plane", 32);
     uint32_t *d_cnt = (uint32_t *)ctx->buf("pl_cnt", 16);
     if (!d_pl || !d_cnt) return LSM_ENOMEM;
+    // the split parts keep the cloud's normals as their prior (select_by_index copies them;
+    // EstimateNormals then orients the new normals to them)
+    const bool carry = c->has_normals;
     for (Cloud *o : {g, r}) {
-        if (hipMalloc(&o->d_raw, size_t(std::max(n, 1)) * 12) != hipSuccess) {
+        if (hipMalloc(&o->d_raw, size_t(std::max(n, 1)) * 12) != hipSuccess ||
+            (carry && hipMalloc(&o->d_prior_ref, size_t(std::max(n, 1)) * 16) != hipSuccess)) {
             ctx->set_error("hipMalloc failed for split cloud");
             return LSM_ENOMEM;
         }
     }
+    float4 *N = nullptr;
+    if (carry && n > 0) {
+        N = (float4 *)ctx->buf("pl_nrm", size_t(n) * 16);
+        if (!N) return LSM_ENOMEM;
+        ref_normals_kernel<<<(n + 255) / 256, 256, 0, st>>>(c->d_nrm, c->d_perm, n, N);
+    }
     LSM_HIP_TRY(ctx, hipMemcpyAsync(d_pl, plane, 32, hipMemcpyHostToDevice, st));
-    split_kernel<<<1, CT, 0, st>>>(P, n, d_pl, thr, g->d_raw, r->d_raw, d_cnt);
+    split_kernel<<<1, CT, 0, st>>>(P, N, n, d_pl, thr, g->d_raw, r->d_raw, g->d_prior_ref,
+                                   r->d_prior_ref, d_cnt);
     uint32_t h[2];
     LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_cnt, 8, hipMemcpyDeviceToHost, st));
     LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
     g->n_raw = h[0];
     r->n_raw = h[1];
+    g->prior_n = carry ? int64_t(h[0]) : 0;
+    r->prior_n = carry ? int64_t(h[1]) : 0;
+    return LSM_OK;
+}
+
+void lsm_ransac_samples(uint64_t seed, int64_t ncorr, int64_t iters, int32_t *out) {
+    for (int64_t k = 0; k < iters * 3; ++k) out[k] = int32_t(splitmix(seed, k) % uint64_t(ncorr));
+}
+
+// RegistrationRANSACBasedOnCorrespondence, sequential form: iterations below the running
+// estimate k are taken in order; a hypothesis that passes the checkers is evaluated by one
+// correspondence pass of the ICP machinery (1-NN within max_corr: fitness, rmse); a better one
+// (fitness, then rmse) lowers k to ceil(log(1 - confidence) / log(1 - ratio^3)).
+int lsm_ransac_run(lsm_ctx *ctx, Cloud *src, Cloud *tgt, const int32_t *corr, int64_t ncorr,
+                   double max_corr, double edge, int64_t iters, double confidence, uint64_t seed,
+                   double T[16], double *fitness, double *rmse, int64_t *evaluated) {
+    hipStream_t st = ctx->stream;
+    for (int k = 0; k < 16; ++k) T[k] = (k % 5 == 0) ? 1.0 : 0.0;
+    *fitness = *rmse = 0.0;
+    *evaluated = 0;
+    if (ncorr < 3 || iters <= 0) return LSM_OK;
+    double *P;
+    int rc;
+    if ((rc = ref_points(ctx, src, &P))) return rc;
+    double *dS = (double *)ctx->buf("rs_src", size_t(std::max<int64_t>(src->n, 1)) * 24);
+    if (!dS) return LSM_ENOMEM;
+    if (src->n > 0)
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(dS, P, size_t(src->n) * 24, hipMemcpyDeviceToDevice, st));
+    if ((rc = ref_points(ctx, tgt, &P))) return rc;   // "pl_P" now holds the target
+    std::vector<int32_t> samples(size_t(iters) * 3);
+    lsm_ransac_samples(seed, ncorr, iters, samples.data());
+    int32_t *d_corr = (int32_t *)ctx->buf("rs_corr", size_t(ncorr) * 8);
+    int32_t *d_s = (int32_t *)ctx->buf("rs_samples", samples.size() * 4);
+    double *d_T = (double *)ctx->buf("rs_T", size_t(iters) * 128);
+    int32_t *d_valid = (int32_t *)ctx->buf("rs_valid", size_t(iters) * 4);
+    double *d_ratio = (double *)ctx->buf("rs_ratio", size_t(iters) * 8);
+    if (!d_corr || !d_s || !d_T || !d_valid || !d_ratio) return LSM_ENOMEM;
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(d_corr, corr, size_t(ncorr) * 8, hipMemcpyHostToDevice, st));
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(d_s, samples.data(), samples.size() * 4, hipMemcpyHostToDevice, st));
+    hipEvent_t ev;
+    ctx->tic("ransac", &ev);
+    ransac_hyp_kernel<<<int((iters + LSM_WAVE - 1) / LSM_WAVE), LSM_WAVE, 0, st>>>(
+        dS, P, d_corr, int(ncorr), d_s, int(iters), max_corr, edge, d_T, d_valid, d_ratio);
+    ctx->toc("ransac", ev);
+    std::vector<int32_t> valid(iters);
+    std::vector<double> ratio(iters), hT(size_t(iters) * 16);
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(valid.data(), d_valid, size_t(iters) * 4, hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(ratio.data(), d_ratio, size_t(iters) * 8, hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(hT.data(), d_T, hT.size() * 8, hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    ctx->collect_timings();
+    lsm_icp_params ip;
+    ip.max_correspondence_distance = max_corr;
+    ip.method = LSM_P2P;
+    ip.max_iteration = 0;
+    ip.relative_fitness = 1e-6;
+    ip.relative_rmse = 1e-6;
+    int64_t est_k = iters;
+    double bfit = 0.0, brmse = 0.0;
+    constexpr int CHUNK = 64;
+    std::vector<lsm_icp_result> res(CHUNK);
+    std::vector<Cloud *> vs(CHUNK, src), vt(CHUNK, tgt);
+    std::vector<double> init(size_t(CHUNK) * 16), efit(static_cast<size_t>(iters)),
+        ermse(static_cast<size_t>(iters));
+    std::vector<char> done(size_t(iters), 0);
+    for (int64_t it = 0; it < iters && it < est_k; ++it) {
+        if (!valid[size_t(it)]) continue;
+        if (!done[size_t(it)]) {
+            // evaluate this and the next valid iterations below the current estimate at once
+            std::vector<int64_t> batch;
+            for (int64_t q = it; q < iters && q < est_k && int(batch.size()) < CHUNK; ++q)
+                if (valid[size_t(q)] && !done[size_t(q)]) batch.push_back(q);
+            for (size_t e = 0; e < batch.size(); ++e)
+                std::memcpy(&init[16 * e], &hT[16 * size_t(batch[e])], 128);
+            if ((rc = lsm_icp_run(ctx, int64_t(batch.size()), vs.data(), vt.data(), init.data(),
+                                  ip, res.data())))
+                return rc;
+            for (size_t e = 0; e < batch.size(); ++e) {
+                done[size_t(batch[e])] = 1;
+                efit[size_t(batch[e])] = res[e].fitness;
+                ermse[size_t(batch[e])] = res[e].inlier_rmse;
+            }
+        }
+        ++*evaluated;
+        const double fit = efit[size_t(it)], rm = ermse[size_t(it)];
+        if (fit > bfit || (fit == bfit && rm < brmse)) {
+            bfit = fit;
+            brmse = rm;
+            std::memcpy(T, &hT[16 * size_t(it)], 128);
+            const double r = ratio[size_t(it)];
+            if (r > 0.0) {
+                const double k = r < 1.0 ? log(1.0 - confidence) / log(1.0 - r * r * r) : 0.0;
+                if (k < double(est_k)) est_k = int64_t(ceil(k));
+            }
+        }
+    }
+    *fitness = bfit;
+    *rmse = brmse;
     return LSM_OK;
 }

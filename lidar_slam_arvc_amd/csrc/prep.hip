@@ -424,19 +424,6 @@ struct Cum {
     int n;
 };
 
-__device__ __forceinline__ void cum_add(Cum &c, const Off &o) {
-    c.sx += o.dx;
-    c.sy += o.dy;
-    c.sz += o.dz;
-    c.sxx += o.xx;
-    c.syy += o.yy;
-    c.szz += o.zz;
-    c.sxy = fma(o.dx, o.dy, c.sxy);
-    c.sxz = fma(o.dx, o.dz, c.sxz);
-    c.syz = fma(o.dy, o.dz, c.syz);
-    c.n += 1;
-}
-
 // Cumulants from the exact f64 offsets of a point (f32 coordinates: the differences are exact).
 // f32 sums were tried: they move some normals by ~1e-6, which is enough to shift chaotic
 // (non-converging) registrations past the transform parity bar.
@@ -454,7 +441,9 @@ __device__ __forceinline__ void cum_add_pt(Cum &c, float4 p, double qx, double q
     c.n += 1;
 }
 
-__device__ __forceinline__ float4 normal_from_cum(const Cum &c) {
+// prior (nullable): EstimateNormals on a cloud that already has normals -- a zero normal keeps
+// the prior one, and the new normal is flipped when it points against the prior.
+__device__ __forceinline__ float4 normal_from_cum(const Cum &c, const float4 *prior = nullptr) {
     sym3 A;
     if (c.n >= 3) {
         const double inv = 1.0 / double(c.n);
@@ -469,7 +458,12 @@ __device__ __forceinline__ float4 normal_from_cum(const Cum &c) {
         A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
     }
     d3 v = fast_eigen3x3_min(A);
-    if (sqrt(d3_dot(v, v)) == 0.0) v = {0.0, 0.0, 1.0};
+    if (sqrt(d3_dot(v, v)) == 0.0) {
+        if (prior) return make_float4(prior->x, prior->y, prior->z, 0.f);
+        v = {0.0, 0.0, 1.0};
+    }
+    if (prior && v.x * double(prior->x) + v.y * double(prior->y) + v.z * double(prior->z) < 0.0)
+        v = {-v.x, -v.y, -v.z};
     return make_float4(float(v.x), float(v.y), float(v.z), 0.f);
 }
 
@@ -609,18 +603,52 @@ __device__ __forceinline__ int sel_classify(const Sel &S, double d2, uint32_t k)
     return b < S.b ? -1 : (b > S.b ? 1 : 0);
 }
 
-// The normal of point j of cloud C by one lane (H: the lane's HSTRIDE-word LDS row).
-__device__ void normal_lane(const CloudDev &C, int j, const NormalParams &np,
-                            unsigned long long *stats, uint32_t *H) {
+// Accumulator policies of hybrid_lane: what is done with the neighbourhood of a point.
+//   add(p, k): neighbour k (sorted index) at p; reset(): drop everything added; finish(): the
+//   neighbourhood is complete.
+// CumAcc: centred f64 cumulants -> the normal (oriented to a prior normal when the cloud has
+// one: EstimateNormals on a cloud with normals, see normal_from_cum).
+struct CumAcc {
+    Cum c;
+    double qx, qy, qz;
+    float4 *out;
+    const float4 *prior;
+    __device__ void add(const float4 &p, uint32_t) { cum_add_pt(c, p, qx, qy, qz); }
+    __device__ void reset() { c = Cum{}; }
+    __device__ void finish() { *out = normal_from_cum(c, prior); }
+};
+
+// ListAcc: the neighbour indices (sorted order) and exact f64 squared distances, unordered.
+struct ListAcc {
+    int32_t *idx;
+    double *d2;
+    int32_t *count;
+    int cap, n;
+    double qx, qy, qz;
+    __device__ void add(const float4 &p, uint32_t k) {
+        if (n < cap) {
+            idx[n] = int32_t(k);
+            d2[n] = lsm_sqdist64(qx, qy, qz, double(p.x), double(p.y), double(p.z));
+        }
+        ++n;
+    }
+    __device__ void reset() { n = 0; }
+    __device__ void finish() { *count = n < cap ? n : cap; }
+};
+
+// KDTreeSearchParamHybrid(radius, max_nn) neighbourhood of point j of cloud C by one lane (H: the
+// lane's HSTRIDE-word LDS row), handed to `acc`.
+template <typename Acc>
+__device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
+                            unsigned long long *stats, uint32_t *H, Acc &acc) {
     uint8_t *H8 = reinterpret_cast<uint8_t *>(H);
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
-    float4 *nrm = const_cast<float4 *>(C.nrm);
 #pragma unroll
     for (int b = 0; b < NB8 / 4; ++b) H[b] = 0;
     Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
     bool sat = false;
-    Cum c = {};
+    int count = 0;
     // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
     // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
     // f32 d^2 and the scale are within 4.2e-7 relative, t < 128). The rest (the sphere's
@@ -640,17 +668,19 @@ __device__ void normal_lane(const CloudDev &C, int j, const NormalParams &np,
                 if (o.d2 < np.r2) bb = sel_level_bin(S, o.d2, k);
             }
             if (bb >= 0) {
-                cum_add_pt(c, p, qx, qy, qz);
+                acc.add(p, k);
+                ++count;
                 const uint32_t v = H8[bb];
                 sat |= v == 255u;
                 H8[bb] = uint8_t(v + (v < 255u ? 1u : 0u));
             }
         });
     });
-    if (c.n <= np.max_nn) {
-        nrm[j] = normal_from_cum(c);
+    if (count <= np.max_nn) {
+        acc.finish();
         return;
     }
+    acc.reset();
     if (stats) atomicAdd(stats, 1ull);   // points that needed the kNN truncation
     double top = np.r2;   // every point below or member has d2 <= top (up to rounding)
     // rescan the members of the current state: their key extremes and a histogram by `next`
@@ -737,7 +767,6 @@ __device__ void normal_lane(const CloudDev &C, int j, const NormalParams &np,
         S = next;
     }
     // final pass: everything below, plus the `need` smallest members
-    Cum f = {};
     uint32_t m = 0;
     ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
@@ -747,7 +776,7 @@ __device__ void normal_lane(const CloudDev &C, int j, const NormalParams &np,
             if (fd >= np.r2_lo && !(o.d2 < np.r2)) return;
             const int cl = sel_classify(S, o.d2, k);
             if (cl < 0) {
-                cum_add(f, o);
+                acc.add(p, k);
             } else if (cl == 0) {
                 if (m < SEL_CAP) {
                     const uint64_t bits = __double_as_longlong(o.d2);
@@ -769,9 +798,9 @@ __device__ void normal_lane(const CloudDev &C, int j, const NormalParams &np,
             // positive doubles order like their bit patterns
             rank += (bg < be || (bg == be && H[3 * g + 2] < ke)) ? 1u : 0u;
         }
-        if (rank < need) cum_add(f, make_off(lsm_ld(C.xyz, ke), qx, qy, qz));
+        if (rank < need) acc.add(lsm_ld(C.xyz, ke), ke);
     }
-    nrm[j] = normal_from_cum(f);
+    acc.finish();
 }
 
 __global__ void __launch_bounds__(PT_THREADS)
@@ -781,316 +810,27 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     const Seg s = segs[blockIdx.x];
     const CloudDev C = cd[s.cloud];
     const int j = s.start + threadIdx.x;
-    if (j < C.n) normal_lane(C, j, np, stats, lds + threadIdx.x * HSTRIDE);
+    if (j >= C.n) return;
+    const float4 q = lsm_ld(C.xyz, j);
+    CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
+               C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
+    hybrid_lane(C, j, np, stats, lds + threadIdx.x * HSTRIDE, acc);
 }
 
-// ------------------------------------------------------------------------------------------
-// normals, split by neighbourhood size
-// ------------------------------------------------------------------------------------------
-// normals_sparse_kernel: one lane per point. The cells a ball can touch bound its size; when
-// that bound is at most dense_t (<= max_nn) the lane scans its ball once (no kNN truncation is
-// possible) and writes the normal. Larger neighbourhoods -- the near field, where balls hold
-// 300 to several thousand points -- go to a queue for normals_dense_kernel: one wave per point,
-// 64 candidates per step from contiguous (coalesced) runs, an LDS histogram per wave and the
-// same exact kNN-300 selection (Sel) as the per-lane path, with every lane of the wave sharing
-// one selection state.
-struct DenseItem {
-    int32_t cloud;
-    int32_t j;
-};
-
-__device__ __forceinline__ void cum_in_ball(Cum &c, const NormalParams &np, float4 qf, double qx,
-                                            double qy, double qz, const float4 &p) {
-    const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
-    const float f = dx * dx + dy * dy + dz * dz;
-    if (f < np.r2_lo) {
-        cum_add_pt(c, p, qx, qy, qz);
-    } else if (f <= np.r2_hi) {
-        const Off o = make_off(p, qx, qy, qz);
-        if (o.d2 < np.r2) cum_add_pt(c, p, qx, qy, qz);
-    }
-}
-
+// Neighbour lists of FPFH (ComputeFPFHFeature's KDTreeSearchParamHybrid): at most `cap` per
+// point, row j of idx / d2 (sorted order), count[j].
 __global__ void __launch_bounds__(PT_THREADS)
-normals_sparse_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, int dense_t,
-                      DenseItem *__restrict__ dq, uint32_t *__restrict__ dqn) {
+nbr_lists_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, int32_t *idx, double *d2,
+                 int32_t *count, int cap) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
     const Seg s = segs[blockIdx.x];
     const CloudDev C = cd[s.cloud];
     const int j = s.start + threadIdx.x;
-    const bool live = j < C.n;
-    bool dense = false;
-    if (live) {
-        const float4 qf = lsm_ld(C.xyz, j);
-        uint32_t bound = 0;
-        ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float, float) { bound += b - a; });
-        dense = bound > uint32_t(dense_t);
-        if (!dense) {
-            const double qx = qf.x, qy = qf.y, qz = qf.z;
-            Cum c = {};
-            ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-                scan_run(C.xyz, a, b, xl, xh,
-                         [&](const float4 &p, uint32_t) { cum_in_ball(c, np, qf, qx, qy, qz, p); });
-            });
-            const_cast<float4 *>(C.nrm)[j] = normal_from_cum(c);
-        }
-    }
-    const uint64_t m = __ballot(dense);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(dqn, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, LSM_WAVE);
-    if (dense) dq[base + __popcll(m & ((uint64_t(1) << lane) - 1))] = {s.cloud, j};
-}
-
-// the per-lane normal of the queued (large-neighbourhood) points: compacted, so every lane of a
-// wave runs the kNN-truncation path
-__global__ void __launch_bounds__(PT_THREADS)
-normals_queue_kernel(const CloudDev *cd, NormalParams np, const DenseItem *__restrict__ dq,
-                     const uint32_t *__restrict__ dqn, unsigned long long *stats) {
-    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
-    const uint32_t total = *dqn;
-    for (uint32_t it = blockIdx.x * PT_THREADS + threadIdx.x; it < total;
-         it += gridDim.x * PT_THREADS) {
-        const DenseItem d = dq[it];
-        normal_lane(cd[d.cloud], d.j, np, stats, lds + threadIdx.x * HSTRIDE);
-    }
-}
-
-// ---- wave-cooperative helpers (every lane of the wave works on the same query point) ----
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-template <typename T>
-__device__ __forceinline__ T wsum(T v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, LSM_WAVE);
-    return v;
-}
-
-__device__ __forceinline__ Cum wave_cum(const Cum &c) {
-    Cum t;
-    t.sx = wsum(c.sx);
-    t.sy = wsum(c.sy);
-    t.sz = wsum(c.sz);
-    t.sxx = wsum(c.sxx);
-    t.sxy = wsum(c.sxy);
-    t.sxz = wsum(c.sxz);
-    t.syy = wsum(c.syy);
-    t.syz = wsum(c.syz);
-    t.szz = wsum(c.szz);
-    t.n = wsum(c.n);
-    return t;
-}
-
-// Every point of the runs a radius-r ball around qf touches, 64 per step: body(p, k, ok) runs on
-// every lane (ok: the lane's point is inside its run's x window). Runs are x-sorted, so a step
-// that reaches past the window ends the run.
-template <typename F>
-__device__ __forceinline__ void wave_ball_visit(const CloudDev &C, float4 qf, float r, F &&body) {
-    const int lane = threadIdx.x & 63;
-    const float *xs = reinterpret_cast<const float *>(C.xyz);
-    ball_visit_runs(C, qf, r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-        uint32_t lo = a, hi = b;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (lsm_ld(xs, size_t(mid) * 4) < xl) lo = mid + 1;
-            else hi = mid;
-        }
-        for (uint32_t base = lo; base < b; base += LSM_WAVE) {
-            const uint32_t k = base + lane;
-            const bool in = k < b;
-            const float4 p = lsm_ld(C.xyz, in ? k : b - 1);
-            body(p, k, in && p.x <= xh);
-            if (__ballot(in && p.x > xh)) break;
-        }
-    });
-}
-
-constexpr int DW = 4;        // waves (dense points in flight) per workgroup
-constexpr int NBR = 128;     // refinement bins (u32 LDS counters per wave)
-constexpr int MCAP = 64;     // final member list: one member per lane
-
-__global__ void __launch_bounds__(DW * LSM_WAVE)
-normals_dense_kernel(const CloudDev *cd, NormalParams np, const DenseItem *__restrict__ dq,
-                     const uint32_t *__restrict__ dqn, unsigned long long *stats) {
-    __shared__ uint32_t hist[DW][NBR];
-    __shared__ double md2[DW][MCAP];
-    __shared__ uint32_t mk[DW][MCAP];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t *H = hist[w];
-    const uint32_t total = *dqn;
-    for (uint32_t it = blockIdx.x * DW + w; it < total; it += gridDim.x * DW) {
-        const DenseItem d = dq[it];
-        const CloudDev C = cd[d.cloud];
-        const float4 qf = lsm_ld(C.xyz, d.j);
-        const double qx = qf.x, qy = qf.y, qz = qf.z;
-        float4 *nrm = const_cast<float4 *>(C.nrm);
-        for (int b = lane; b < NBR; b += LSM_WAVE) H[b] = 0;
-        wave_sync();
-        // pass 1: count, cumulants and the level-0 histogram (128 bins of d2 over [0, r^2));
-        // f32 decisions where they are certain, the exact f64 distance otherwise (see
-        // normals_kernel)
-        Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
-        Cum c = {};
-        wave_ball_visit(C, qf, np.r, [&](const float4 &p, uint32_t k, bool ok) {
-            if (!ok) return;
-            const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
-            const float f = dx * dx + dy * dy + dz * dz;
-            const float t = f * np.hscale;
-            const float fr = t - floorf(t);
-            int bb = -1;
-            if (f < np.r2_lo && fr > 2e-4f && fr < 1.f - 2e-4f) {
-                bb = int(t);
-            } else if (f <= np.r2_hi) {
-                const Off o = make_off(p, qx, qy, qz);
-                if (o.d2 < np.r2) bb = sel_level_bin(S, o.d2, k);
-            }
-            if (bb >= 0) {
-                cum_add_pt(c, p, qx, qy, qz);
-                atomicAdd(&H[bb], 1u);
-            }
-        });
-        const int count = wsum(c.n);
-        if (count <= np.max_nn) {
-            const Cum t = wave_cum(c);
-            if (lane == 0) nrm[d.j] = normal_from_cum(t);
-            continue;
-        }
-        if (stats && lane == 0) atomicAdd(stats, 1ull);
-        double top = np.r2;
-        uint32_t need = uint32_t(np.max_nn);
-        for (int lev = 0; lev < MAX_REFINE; ++lev) {
-            wave_sync();
-            // first bin whose running count reaches `need`: two bins per lane, wave scan
-            const int nb = S.nb;
-            const int b0 = 2 * lane, b1 = 2 * lane + 1;
-            const uint32_t h0 = b0 < nb ? H[b0] : 0u, h1 = b1 < nb ? H[b1] : 0u;
-            uint32_t incl = h0 + h1;
-#pragma unroll
-            for (int off = 1; off < LSM_WAVE; off <<= 1) {
-                const uint32_t y = __shfl_up(incl, off, LSM_WAVE);
-                if (lane >= off) incl += y;
-            }
-            const uint32_t excl = incl - h0 - h1;
-            // this lane's bin reaching `need` first (at most one lane's first crossing)
-            int mine = -1;
-            uint32_t acc_l = 0;
-            if (b0 < nb && excl + h0 >= need && excl < need) {
-                mine = b0;
-                acc_l = excl;
-            } else if (b1 < nb && excl + h0 + h1 >= need && excl + h0 < need) {
-                mine = b1;
-                acc_l = excl + h0;
-            }
-            const uint64_t hit = __ballot(mine >= 0);
-            int bstar = nb - 1;
-            uint32_t acc = 0;
-            if (hit) {
-                const int src = __ffsll((unsigned long long)hit) - 1;
-                bstar = __shfl(mine, src, LSM_WAVE);
-                acc = __shfl(acc_l, src, LSM_WAVE);
-            } else {   // fewer than `need` in total: take everything (cannot happen: count > max_nn)
-                acc = __shfl(incl, LSM_WAVE - 1, LSM_WAVE) - H[nb - 1];
-            }
-            const uint32_t bin_count = H[bstar];
-            need -= acc;
-            S.b = bstar;
-            if (!S.by_idx) top = fmin(top, S.lo + double(bstar + 1) / S.scale);
-            if (bin_count <= uint32_t(MCAP)) break;
-            // next level over the chosen bin's range, clipped to the members' exact extremes
-            Sel next = S;
-            {
-                const double vlo = S.by_idx ? double(S.klo) : S.dlo;
-                const double vhi = S.by_idx ? double(S.khi) + 1.0 : S.dhi;
-                const double elo = fmax(S.lo + double(bstar) / S.scale, vlo);
-                const double ehi = fmin(S.lo + double(bstar + 1) / S.scale, vhi);
-                next.lo = elo;
-                next.scale = ehi > elo ? double(NBR) / (ehi - elo) : S.scale * double(NBR);
-                next.nb = NBR;
-            }
-            double dmin, dmax;
-            uint32_t kmin, kmax;
-            auto refine = [&](const Sel &lv) {
-                wave_sync();
-                for (int b = lane; b < NBR; b += LSM_WAVE) H[b] = 0;
-                wave_sync();
-                double lmin = INFINITY, lmax = -INFINITY;
-                uint32_t kl = 0xffffffffu, kh = 0u;
-                wave_ball_visit(C, qf, sel_radius(top, np.r), [&](const float4 &p, uint32_t k, bool ok) {
-                    Off o;
-                    if (ok && in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
-                        atomicAdd(&H[sel_level_bin(lv, o.d2, k)], 1u);
-                        lmin = fmin(lmin, o.d2);
-                        lmax = fmax(lmax, o.d2);
-                        kl = min(kl, k);
-                        kh = max(kh, k);
-                    }
-                });
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) {
-                    lmin = fmin(lmin, __shfl_xor(lmin, off, LSM_WAVE));
-                    lmax = fmax(lmax, __shfl_xor(lmax, off, LSM_WAVE));
-                    kl = min(kl, (uint32_t)__shfl_xor((int)kl, off, LSM_WAVE));
-                    kh = max(kh, (uint32_t)__shfl_xor((int)kh, off, LSM_WAVE));
-                }
-                dmin = lmin;
-                dmax = lmax;
-                kmin = kl;
-                kmax = kh;
-            };
-            refine(next);
-            if (!S.by_idx && dmin == dmax) {
-                // every member has the same d2: order them by index instead
-                next.by_idx = 1;
-                next.lo = double(kmin);
-                next.scale = double(NBR) / (double(kmax - kmin) + 1.0);
-                refine(next);
-            }
-            next.dlo = dmin;
-            next.dhi = dmax;
-            next.klo = next.by_idx ? kmin : 0u;
-            next.khi = next.by_idx ? kmax : 0xffffffffu;
-            top = fmin(top, dmax);
-            S = next;
-        }
-        // final pass: everything below, plus the `need` smallest members by (d2, k)
-        wave_sync();
-        Cum f = {};
-        uint32_t m = 0;
-        wave_ball_visit(C, qf, sel_radius(top, np.r), [&](const float4 &p, uint32_t k, bool ok) {
-            Off o;
-            const bool in = ok && in_ball(np, qf, qx, qy, qz, p, o);
-            const int cl = in ? sel_classify(S, o.d2, k) : 1;
-            if (cl < 0) cum_add_pt(f, p, qx, qy, qz);
-            const uint64_t mm = __ballot(cl == 0);
-            if (cl == 0) {
-                const uint32_t slot = m + __popcll(mm & ((uint64_t(1) << lane) - 1));
-                if (slot < uint32_t(MCAP)) {
-                    md2[w][slot] = o.d2;
-                    mk[w][slot] = k;
-                }
-            }
-            m += __popcll(mm);
-        });
-        wave_sync();
-        const uint32_t M = m < uint32_t(MCAP) ? m : uint32_t(MCAP);
-        if (uint32_t(lane) < M) {
-            const double de = md2[w][lane];
-            const uint32_t ke = mk[w][lane];
-            uint32_t rank = 0;
-            for (uint32_t g = 0; g < M; ++g) {
-                const double dg = md2[w][g];
-                rank += (dg < de || (dg == de && mk[w][g] < ke)) ? 1u : 0u;
-            }
-            if (rank < need) cum_add_pt(f, lsm_ld(C.xyz, ke), qx, qy, qz);
-        }
-        const Cum t = wave_cum(f);
-        if (lane == 0) nrm[d.j] = normal_from_cum(t);
-    }
+    if (j >= C.n) return;
+    const float4 q = lsm_ld(C.xyz, j);
+    ListAcc acc{idx + size_t(j) * cap, d2 + size_t(j) * cap, count + j, cap, 0,
+                double(q.x), double(q.y), double(q.z)};
+    hybrid_lane(C, j, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1491,6 +1231,9 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         D.nby = geo[k].nby;
         D.nbz = geo[k].nbz;
         D.n = int(wn[k]);
+        D.perm = c->d_perm;
+        D.prior_ref = (p.want_normals && c->d_prior_ref && c->prior_n == int64_t(wn[k]))
+                          ? c->d_prior_ref : nullptr;
         perm_ptrs[k] = c->d_perm;
         cell_ptrs[k] = c->d_cell;
     }
@@ -1555,41 +1298,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 d_ns = (unsigned long long *)ctx->buf("n_stats", 8 * 8);
                 LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 64, st));
             }
-            // default: one lane per point in place (cell-sorted order keeps a wave's points
-            // together). LSM_NORMALS_SPLIT=1: sparse kernel + queue of the large
-            // neighbourhoods (per lane, or one wave per point with LSM_NORMALS_WAVE=1) --
-            // measured slower, kept for experiments.
-            static const bool legacy = getenv("LSM_NORMALS_SPLIT") == nullptr &&
-                                       getenv("LSM_NORMALS_WAVE") == nullptr;
-            static const int dense_env = [] {
-                const char *e = getenv("LSM_NORMALS_DENSE_T");
-                return e ? atoi(e) : 128;
-            }();
-            if (legacy) {
-                normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
-            } else {
-                const int dense_t = std::max(0, std::min(dense_env, np.max_nn));
-                int64_t total_pts = 0;
-                for (uint32_t v : wn) total_pts += v;
-                DenseItem *d_dq = (DenseItem *)ctx->buf(
-                    "n_dq", size_t(std::max<int64_t>(total_pts, 1)) * sizeof(DenseItem));
-                uint32_t *d_dqn = (uint32_t *)ctx->buf("n_dqn", 4);
-                if (!d_dq || !d_dqn) return LSM_ENOMEM;
-                LSM_HIP_TRY(ctx, hipMemsetAsync(d_dqn, 0, 4, st));
-                normals_sparse_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np,
-                                                                              dense_t, d_dq, d_dqn);
-                static const bool wave_dense = getenv("LSM_NORMALS_WAVE") != nullptr;
-                if (wave_dense) {
-                    const int dgrid = std::max(1, ctx->num_cus * 8);
-                    normals_dense_kernel<<<dgrid, DW * LSM_WAVE, 0, st>>>(d_cd, np, d_dq, d_dqn,
-                                                                         d_ns);
-                } else {
-                    const int qgrid = int(std::max<int64_t>(1, std::min<int64_t>(
-                        (total_pts + PT_THREADS - 1) / PT_THREADS, int64_t(ctx->num_cus) * 16)));
-                    normals_queue_kernel<<<qgrid, PT_THREADS, 0, st>>>(d_cd, np, d_dq, d_dqn,
-                                                                       d_ns);
-                }
-            }
+            normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
             if (nstats) {
                 unsigned long long h = 0;
                 LSM_HIP_TRY(ctx, hipMemcpyAsync(&h, d_ns, 8, hipMemcpyDeviceToHost, st));
@@ -1638,5 +1347,287 @@ int lsm_download_run(lsm_ctx *ctx, Cloud *c, double *xyz, double *nrm, int64_t c
     }
     if (nrm) LSM_HIP_TRY(ctx, hipMemcpyAsync(nrm, dn, size_t(n) * 24, hipMemcpyDeviceToHost, st));
     LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    return LSM_OK;
+}
+
+// ==========================================================================================
+// FPFH: [O3D] ComputeFPFHFeature(cloud, KDTreeSearchParamHybrid(r, max_nn))
+// ==========================================================================================
+namespace {
+
+// ComputePairFeatures (Rusu's Darboux frame), f64: (theta, alpha, phi); false when the points
+// coincide or the frame degenerates (Open3D returns zeros then).
+__device__ bool pair_features(const double *p1, const double *n1, const double *p2,
+                              const double *n2, double f[3]) {
+    double dp[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    const double d = sqrt((dp[0] * dp[0] + dp[1] * dp[1]) + dp[2] * dp[2]);
+    f[0] = f[1] = f[2] = 0.0;
+    if (d == 0.0) return false;
+    const double a1 = ((n1[0] * dp[0] + n1[1] * dp[1]) + n1[2] * dp[2]) / d;
+    const double a2 = ((n2[0] * dp[0] + n2[1] * dp[1]) + n2[2] * dp[2]) / d;
+    const double *m1 = n1, *m2 = n2;
+    double phi = a1;
+    if (acos(fabs(a1)) > acos(fabs(a2))) {
+        m1 = n2;
+        m2 = n1;
+        dp[0] = -dp[0];
+        dp[1] = -dp[1];
+        dp[2] = -dp[2];
+        phi = -a2;
+    }
+    double v[3] = {dp[1] * m1[2] - dp[2] * m1[1], dp[2] * m1[0] - dp[0] * m1[2],
+                   dp[0] * m1[1] - dp[1] * m1[0]};
+    const double vn = sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+    if (vn == 0.0) return false;
+    v[0] /= vn;
+    v[1] /= vn;
+    v[2] /= vn;
+    const double w[3] = {m1[1] * v[2] - m1[2] * v[1], m1[2] * v[0] - m1[0] * v[2],
+                         m1[0] * v[1] - m1[1] * v[0]};
+    f[1] = (v[0] * m2[0] + v[1] * m2[1]) + v[2] * m2[2];
+    f[0] = atan2((w[0] * m2[0] + w[1] * m2[1]) + w[2] * m2[2],
+                 (m1[0] * m2[0] + m1[1] * m2[1]) + m1[2] * m2[2]);
+    f[2] = phi;
+    return true;
+}
+
+__device__ __forceinline__ int fbin(double v) {
+    const int h = int(floor(v));
+    return h < 0 ? 0 : (h >= 11 ? 10 : h);
+}
+
+// SPFH of every point: the pairs (point, neighbour) over its list without the point itself,
+// 11 bins each of theta, alpha, phi, increment 100 / (k - 1) (k counts the point itself)
+__global__ void __launch_bounds__(PT_THREADS)
+spfh_kernel(const CloudDev *cd, const int32_t *__restrict__ idx, const int32_t *__restrict__ cnt,
+            int cap, double *__restrict__ spfh) {
+    const CloudDev C = cd[0];
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= C.n) return;
+    double h[33];
+#pragma unroll
+    for (int b = 0; b < 33; ++b) h[b] = 0.0;
+    const int k = cnt[j];
+    if (k > 1) {
+        const double incr = 100.0 / double(k - 1);
+        const float4 pj = C.xyz[j], nj = C.nrm[j];
+        const double p1[3] = {pj.x, pj.y, pj.z}, n1[3] = {nj.x, nj.y, nj.z};
+        for (int e = 0; e < k; ++e) {
+            const int q = idx[size_t(j) * cap + e];
+            if (q == j) continue;
+            const float4 pq = C.xyz[q], nq = C.nrm[q];
+            const double p2[3] = {pq.x, pq.y, pq.z}, n2[3] = {nq.x, nq.y, nq.z};
+            double f[3];
+            pair_features(p1, n1, p2, n2, f);
+            const double twopi = 2.0 * 3.14159265358979323846;
+            const int b0 = fbin(11.0 * (f[0] + 3.14159265358979323846) / twopi);
+            const int b1 = fbin(11.0 * (f[1] + 1.0) * 0.5);
+            const int b2 = fbin(11.0 * (f[2] + 1.0) * 0.5);
+#pragma unroll
+            for (int b = 0; b < 11; ++b) {
+                h[b] += b == b0 ? incr : 0.0;
+                h[11 + b] += b == b1 ? incr : 0.0;
+                h[22 + b] += b == b2 ? incr : 0.0;
+            }
+        }
+    }
+    for (int b = 0; b < 33; ++b) spfh[size_t(j) * 33 + b] = h[b];
+}
+
+// FPFH = SPFH(j) + the neighbours' SPFH weighted by 1 / d^2 and normalised to 100 per group of
+// 11 bins; written in reference order (row perm[j]).
+__global__ void __launch_bounds__(PT_THREADS)
+fpfh_kernel(const CloudDev *cd, const int32_t *__restrict__ idx, const double *__restrict__ d2,
+            const int32_t *__restrict__ cnt, int cap, const double *__restrict__ spfh,
+            double *__restrict__ out) {
+    const CloudDev C = cd[0];
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= C.n) return;
+    double acc[33];
+#pragma unroll
+    for (int b = 0; b < 33; ++b) acc[b] = 0.0;
+    const int k = cnt[j];
+    double *o = out + size_t(C.perm[j]) * 33;
+    if (k <= 1) {
+        for (int b = 0; b < 33; ++b) o[b] = 0.0;
+        return;
+    }
+    for (int e = 0; e < k; ++e) {
+        const int q = idx[size_t(j) * cap + e];
+        const double dd = d2[size_t(j) * cap + e];
+        if (q == j || dd == 0.0) continue;
+        const double *sq = spfh + size_t(q) * 33;
+#pragma unroll
+        for (int b = 0; b < 33; ++b) acc[b] += sq[b] / dd;
+    }
+    double s[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int b = 0; b < 33; ++b) s[b / 11] += acc[b];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) s[g] = s[g] != 0.0 ? 100.0 / s[g] : 0.0;
+    const double *sj = spfh + size_t(j) * 33;
+#pragma unroll
+    for (int b = 0; b < 33; ++b) o[b] = acc[b] * s[b / 11] + sj[b];
+}
+
+// Exact nearest feature (33-D, squared L2 summed in dimension order; ties -> lower index): one
+// thread per query row, target rows staged through LDS in tiles.
+constexpr int FT = 64;
+__global__ void __launch_bounds__(PT_THREADS)
+feature_nn_kernel(const double *__restrict__ a, int na, const double *__restrict__ b, int nb,
+                  int32_t *__restrict__ nn) {
+    __shared__ double tile[FT * 33];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double q[33];
+    if (i < na)
+        for (int d = 0; d < 33; ++d) q[d] = a[size_t(i) * 33 + d];
+    double best = INFINITY;
+    int bi = -1;
+    for (int t0 = 0; t0 < nb; t0 += FT) {
+        const int m = min(FT, nb - t0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < m * 33; e += blockDim.x) tile[e] = b[size_t(t0) * 33 + e];
+        __syncthreads();
+        if (i < na) {
+            for (int r = 0; r < m; ++r) {
+                double s = 0.0;
+#pragma unroll
+                for (int d = 0; d < 33; ++d) {
+                    const double e = q[d] - tile[r * 33 + d];
+                    s += e * e;
+                }
+                if (s < best) {
+                    best = s;
+                    bi = t0 + r;
+                }
+            }
+        }
+    }
+    if (i < na) nn[i] = bi;
+}
+
+// mutual filter: keep (i, ij[i]) when ji[ij[i]] == i, in increasing i (one workgroup)
+__global__ void __launch_bounds__(1024)
+mutual_kernel(const int32_t *__restrict__ ij, int na, const int32_t *__restrict__ ji,
+              int32_t *__restrict__ out, uint32_t *__restrict__ nout) {
+    __shared__ uint32_t wcnt[1024 / LSM_WAVE];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t carry = 0;
+    for (int base = 0; base < na; base += 1024) {
+        const int i = base + int(threadIdx.x);
+        const bool on = i < na && ij[i] >= 0 && ji[ij[i]] == i;
+        const uint64_t m = __ballot(on);
+        if (lane == 0) wcnt[w] = __popcll(m);
+        __syncthreads();
+        uint32_t before = carry, tot = 0;
+        for (int q = 0; q < 1024 / LSM_WAVE; ++q) {
+            before += q < w ? wcnt[q] : 0u;
+            tot += wcnt[q];
+        }
+        if (on) {
+            const uint32_t slot = before + __popcll(m & ((uint64_t(1) << lane) - 1));
+            out[2 * slot] = i;
+            out[2 * slot + 1] = ij[i];
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *nout = carry;
+}
+
+}  // namespace
+
+int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn) {
+    hipStream_t st = ctx->stream;
+    const int n = int(c->n);
+    if (!c->d_fpfh || c->fpfh_cap < n) {
+        (void)hipFree(c->d_fpfh);
+        c->d_fpfh = nullptr;
+        if (hipMalloc(&c->d_fpfh, size_t(std::max(n, 1)) * 33 * 8) != hipSuccess) {
+            ctx->set_error("hipMalloc failed for FPFH features");
+            return LSM_ENOMEM;
+        }
+        c->fpfh_cap = std::max(n, 1);
+    }
+    c->fpfh_n = n;
+    if (n == 0) return LSM_OK;
+    const int cap = std::max(max_nn, 1);
+    int32_t *d_idx = (int32_t *)ctx->buf("fp_idx", size_t(n) * cap * 4);
+    double *d_d2 = (double *)ctx->buf("fp_d2", size_t(n) * cap * 8);
+    int32_t *d_cnt = (int32_t *)ctx->buf("fp_cnt", size_t(n) * 4);
+    double *d_spfh = (double *)ctx->buf("fp_spfh", size_t(n) * 33 * 8);
+    if (!d_idx || !d_d2 || !d_cnt || !d_spfh) return LSM_ENOMEM;
+    std::vector<CloudDev> cdv(1, c->dev);
+    cdv[0].nrm = c->d_nrm;
+    CloudDev *d_cd;
+    int rc;
+    if ((rc = upload_vec(ctx, "fp_cd", cdv, &d_cd))) return rc;
+    std::vector<Seg> segs = point_segments(std::vector<uint32_t>(1, uint32_t(n)), PT_THREADS);
+    Seg *d_segs;
+    if ((rc = upload_vec(ctx, "fp_segs", segs, &d_segs))) return rc;
+    NormalParams np;
+    np.r2 = radius * radius;
+    np.r = float(radius);
+    np.r2_lo = float(np.r2 * (1.0 - 4e-6));
+    np.r2_hi = float(np.r2 * (1.0 + 4e-6));
+    np.hscale = float(double(NB8) / np.r2);
+    np.max_nn = max_nn;
+    hipEvent_t ev;
+    ctx->tic("fpfh", &ev);
+    nbr_lists_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_idx, d_d2, d_cnt,
+                                                              cap);
+    const int g = (n + PT_THREADS - 1) / PT_THREADS;
+    spfh_kernel<<<g, PT_THREADS, 0, st>>>(d_cd, d_idx, d_cnt, cap, d_spfh);
+    fpfh_kernel<<<g, PT_THREADS, 0, st>>>(d_cd, d_idx, d_d2, d_cnt, cap, d_spfh, c->d_fpfh);
+    ctx->toc("fpfh", ev);
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    LSM_HIP_TRY(ctx, hipGetLastError());
+    ctx->collect_timings();
+    return LSM_OK;
+}
+
+int lsm_feature_corr_run(lsm_ctx *ctx, Cloud *s, Cloud *t, int mutual, int ransac_n,
+                         int32_t *out, int64_t cap, int64_t *n_out) {
+    hipStream_t st = ctx->stream;
+    const int na = int(s->fpfh_n), nb = int(t->fpfh_n);
+    int32_t *d_ij = (int32_t *)ctx->buf("fc_ij", size_t(std::max(na, 1)) * 4);
+    int32_t *d_ji = (int32_t *)ctx->buf("fc_ji", size_t(std::max(nb, 1)) * 4);
+    int32_t *d_out = (int32_t *)ctx->buf("fc_out", size_t(std::max(na, 1)) * 8);
+    uint32_t *d_n = (uint32_t *)ctx->buf("fc_n", 4);
+    if (!d_ij || !d_ji || !d_out || !d_n) return LSM_ENOMEM;
+    *n_out = 0;
+    if (na == 0 || nb == 0) return LSM_OK;
+    hipEvent_t ev;
+    ctx->tic("feature_nn", &ev);
+    feature_nn_kernel<<<(na + PT_THREADS - 1) / PT_THREADS, PT_THREADS, 0, st>>>(s->d_fpfh, na,
+                                                                               t->d_fpfh, nb, d_ij);
+    std::vector<int32_t> h;
+    uint32_t nm = 0;
+    if (mutual) {
+        feature_nn_kernel<<<(nb + PT_THREADS - 1) / PT_THREADS, PT_THREADS, 0, st>>>(
+            t->d_fpfh, nb, s->d_fpfh, na, d_ji);
+        mutual_kernel<<<1, 1024, 0, st>>>(d_ij, na, d_ji, d_out, d_n);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(&nm, d_n, 4, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    }
+    ctx->toc("feature_nn", ev);
+    if (mutual && int64_t(nm) >= int64_t(3) * ransac_n) {
+        h.resize(size_t(nm) * 2);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(h.data(), d_out, h.size() * 4, hipMemcpyDeviceToHost, st));
+    } else {   // too few mutual pairs (or no filter): every source feature's nearest
+        std::vector<int32_t> ij(na);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(ij.data(), d_ij, size_t(na) * 4, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        h.resize(size_t(na) * 2);
+        for (int i = 0; i < na; ++i) {
+            h[2 * i] = i;
+            h[2 * i + 1] = ij[i];
+        }
+    }
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    ctx->collect_timings();
+    const int64_t m = int64_t(h.size() / 2);
+    *n_out = m;
+    if (out) std::memcpy(out, h.data(), size_t(std::min(m, cap)) * 8);
     return LSM_OK;
 }

@@ -11,16 +11,20 @@ behind them are replaced by liblidarsm (include/lidarsm.h) through ctypes:
     preprocess_icp2planes      keyframe.py:164-189  lsm_ground_plane (RANSAC) + lsm_split_plane +
                                                     normals of both parts
     local_registration_two_planes keyframe.py:262-295  two P2Plane ICPs in one batch, composed
+    preprocess_fpfh            keyframe.py:191-229  icp2planes pre-processing + lsm_fpfh (§8f row 4)
+    global_registration        keyframe.py:296-345  lsm_feature_correspondences + lsm_ransac_feature
+                                                    + P2Plane refinement
 
 ``pointcloud`` / ``pointcloud_filtered`` expose ``.points`` (N x 3 float64) and ``.normals`` like
 the o3d.geometry.PointCloud the reference kept, downloaded lazily from the device cache.
 
 Deliberate divergences: an unknown ``option`` raises ValueError (the
-reference hits UnboundLocalError, keyframe.py:253-255); 'fpfh' pre-processing (keyframe.py:191-229)
-raises NotImplementedError; ``transform`` returns a transformed host copy
-instead of mutating the device-resident filtered cloud; the RANSAC of 'icp2planes' samples from
-splitmix64(``ransac_seed``) where Open3D uses its unseeded RNG, and ``segment_plane`` returns the
-two parts with their final normals (r = 0.5 ground / 0.3 rest) already estimated.
+reference hits UnboundLocalError, keyframe.py:253-255); ``transform`` returns a transformed host
+copy instead of mutating the device-resident filtered cloud; both RANSACs ('icp2planes' plane,
+'fpfh' feature matching) sample from splitmix64(``ransac_seed``) where Open3D uses its unseeded
+RNG, and ``segment_plane`` returns the two parts with their final normals (r = 0.5 ground / 0.3
+rest) already estimated; 'fpfh' with a voxel_size (the reference voxelises twice,
+keyframe.py:193-203) raises NotImplementedError.
 """
 from __future__ import annotations
 
@@ -57,6 +61,21 @@ class HostPointCloud:
         if self.has_normals():
             self.normals = self.normals @ T[:3, :3].T
         return self
+
+
+class FeatureHandle:
+    """The FPFH features of a device cloud (o3d Feature: ``.data`` 33 x N), fetched lazily."""
+
+    def __init__(self, dev, handle):
+        self._dev = dev
+        self._handle = handle
+        self._data = None
+
+    @property
+    def data(self):
+        if self._data is None:
+            self._data = self._dev.fpfh(self._handle, 0.3, 100).T
+        return self._data
 
 
 class DevicePointCloud:
@@ -228,8 +247,33 @@ class KeyFrame:
         elif method == "icp2planes":
             self.preprocess_icp2planes()
         elif method == "fpfh":
-            raise NotImplementedError("pre-processing method 'fpfh' is not on the MI355X path "
-                                      "yet (SURVEY.md §8f row 4)")
+            self.preprocess_fpfh()
+
+    # ------------------------------------------------------------------ FPFH (§8f row 4)
+    def preprocess_fpfh(self):
+        if self.voxel_size is not None:
+            raise NotImplementedError("'fpfh' with a voxel_size (the reference voxelises twice, "
+                                      "keyframe.py:193-203) is not on the MI355X path")
+        self.preprocess_icp2planes()        # filter, normals, plane, split, part normals
+        self._dev.fpfh(self._planes[1], self.voxel_size_normals, 100, download=False)
+        self.pointcloud_fpfh = FeatureHandle(self._dev, self._planes[1])
+
+    def global_registration(self, other):
+        """RANSAC on the non-ground parts' FPFH matches, then P2Plane ICP of the filtered clouds
+        from its result (keyframe.py:296-345)."""
+        for kf in (self, other):
+            if kf.pointcloud_fpfh is None:
+                raise RuntimeError("global_registration needs pre_process('fpfh') on both keyframes")
+        src, tgt = other._planes[1], self._planes[1]
+        corres = self._dev.feature_correspondences(src, tgt, mutual=True, ransac_n=3)
+        r = self._dev.ransac_feature(src, tgt, corres, self.fpfh_threshold, 0.9, 100000, 0.999,
+                                     seed=self.ransac_seed)
+        self.last_ransac = r
+        res = self._dev.icp_batch([other._handle], [self._handle],
+                                  r["transformation"].reshape(1, 16),
+                                  self.registration_params("pointplane"))[0]
+        self.last_registration = res
+        return HomogeneousMatrix(res["transformation"])
 
     # ------------------------------------------------------------------ two planes (§8f row 2)
     def preprocess_icp2planes(self):

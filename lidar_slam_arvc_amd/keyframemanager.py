@@ -9,9 +9,9 @@ Same constructor and methods (add_keyframes :20-24, add_keyframe :26-30, load_po
   (scan-matcher chain, loop-closure candidates).
 
 ``compute_transformation`` dispatches on ``method`` exactly like the reference: 'icppointpoint'
--> P2P, 'icppointplane' -> P2Plane, 'icp2planes' -> local_registration_two_planes (:66-67);
-'fpfh' is not on the device path yet and raises NotImplementedError; an
-unknown method prints and returns None, as in the reference (:70-72).
+-> P2P, 'icppointplane' -> P2Plane, 'icp2planes' -> local_registration_two_planes (:66-67),
+'fpfh' -> global_registration (:68-69); an unknown method prints and returns None, as in the
+reference (:70-72).
 """
 from __future__ import annotations
 
@@ -83,8 +83,7 @@ class KeyFrameManager:
             transform = self.keyframes[i].local_registration_two_planes(
                 self.keyframes[j], initial_transform=Tij.array)
         elif self.method == "fpfh":
-            raise NotImplementedError("registration method 'fpfh' is not on the MI355X path yet "
-                                      "(SURVEY.md §8f row 4)")
+            transform = self.keyframes[i].global_registration(self.keyframes[j])
         else:
             print("Unknown registration method")
             transform = None

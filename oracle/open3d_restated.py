@@ -648,3 +648,201 @@ def registration_two_planes(src, tgt, init=None, max_corr=DISTANCE_THRESHOLD):
     t2 = HomogeneousMatrix(rb["transformation"]).t2v(n=3)
     T = HomogeneousMatrix(np.array([t2[0], t2[1], t1[2]]), Euler([t1[3], t1[4], t2[5]]))
     return T.array, ra, rb
+
+
+# --------------------------------------------------------------------------------------------
+# §8f row 4, 'fpfh': preprocess_fpfh (keyframe.py:191-229) and global_registration (:296-345):
+# [O3D] EstimateNormals with prior normals, ComputeFPFHFeature, and
+# RegistrationRANSACBasedOnFeatureMatching (mutual filter, P2P without scaling, ransac_n = 3,
+# edge-length 0.9 and distance checkers, RANSACConvergenceCriteria(100000, 0.999)), then the
+# P2Plane refinement on the filtered clouds.
+# --------------------------------------------------------------------------------------------
+def estimate_normals_oriented(points, prior, radius=NORMAL_RADIUS, max_nn=MAX_NN):
+    """EstimateNormals on a cloud that already has normals: a zero normal keeps the prior one and
+    every new normal is flipped to agree with its prior (normal . prior < 0 -> -normal)."""
+    p = np.asarray(points, dtype=np.float64)
+    tree = cKDTree(p)
+    idx, _, cnt = hybrid_search(tree, p, p, radius, max_nn)
+    n = fast_eigen3x3(compute_covariance(p, idx, cnt))
+    prior = np.asarray(prior, dtype=np.float64)
+    zero = np.sqrt(_dot(n, n)) == 0.0
+    n[zero] = prior[zero]
+    flip = _dot(n, prior) < 0.0
+    n[flip] *= -1.0
+    return n
+
+
+def _pair_features(p1, n1, p2, n2):
+    """ComputePairFeatures (Rusu's Darboux frame): (theta, alpha, phi, d) per pair; zero rows
+    where the points coincide or the frame degenerates."""
+    dp = p2 - p1
+    d = np.sqrt(_dot(dp, dp))
+    bad = d == 0.0
+    ds = np.where(bad, 1.0, d)
+    a1 = _dot(n1, dp) / ds
+    a2 = _dot(n2, dp) / ds
+    swap = np.arccos(np.abs(a1)) > np.arccos(np.abs(a2))
+    n1c = np.where(swap[:, None], n2, n1)
+    n2c = np.where(swap[:, None], n1, n2)
+    dp = np.where(swap[:, None], -dp, dp)
+    f2 = np.where(swap, -a2, a1)
+    v = _cross(dp, n1c)
+    vn = np.sqrt(_dot(v, v))
+    bad |= vn == 0.0
+    v = v / np.where(vn == 0.0, 1.0, vn)[:, None]
+    w = _cross(n1c, v)
+    f1 = _dot(v, n2c)
+    f0 = np.arctan2(_dot(w, n2c), _dot(n1c, n2c))
+    z = np.zeros_like(f0)
+    return np.where(bad, z, f0), np.where(bad, z, f1), np.where(bad, z, f2)
+
+
+def compute_fpfh(points, normals, radius=0.3, max_nn=100):
+    """ComputeFPFHFeature: SPFH over each point's hybrid neighbourhood without the point itself
+    (11 bins each of theta, alpha, phi; increments 100 / (k - 1)), then FPFH = SPFH(i) +
+    normalised sum of the neighbours' SPFH / d^2. Returns N x 33."""
+    p = np.asarray(points, dtype=np.float64)
+    nr = np.asarray(normals, dtype=np.float64)
+    n = len(p)
+    tree = cKDTree(p)
+    idx, d2, cnt = hybrid_search(tree, p, p, radius, max_nn)
+    rows = np.repeat(np.arange(n), idx.shape[1])
+    cols = idx.reshape(-1)
+    dd = d2.reshape(-1)
+    ok = (cols >= 0) & (cols != rows)          # the point itself is skipped
+    rows, cols, dd = rows[ok], cols[ok], dd[ok]
+    spfh = np.zeros((n, 33))
+    has = cnt > 1
+    incr = np.where(has, 100.0 / np.maximum(cnt - 1, 1), 0.0)
+    f0, f1, f2 = _pair_features(p[rows], nr[rows], p[cols], nr[cols])
+    h0 = np.clip(np.floor(11 * (f0 + math.pi) / (2.0 * math.pi)).astype(np.int64), 0, 10)
+    h1 = np.clip(np.floor(11 * (f1 + 1.0) * 0.5).astype(np.int64), 0, 10)
+    h2 = np.clip(np.floor(11 * (f2 + 1.0) * 0.5).astype(np.int64), 0, 10)
+    w = incr[rows]
+    np.add.at(spfh, (rows, h0), w)
+    np.add.at(spfh, (rows, h1 + 11), w)
+    np.add.at(spfh, (rows, h2 + 22), w)
+    nz = dd != 0.0
+    r2, c2, d2n = rows[nz], cols[nz], dd[nz]
+    acc = np.zeros((n, 33))
+    np.add.at(acc, r2, spfh[c2] / d2n[:, None])
+    s = acc.reshape(n, 3, 11).sum(axis=2)
+    scale = np.where(s != 0.0, 100.0 / np.where(s != 0.0, s, 1.0), 0.0)
+    fpfh = acc * np.repeat(scale, 11, axis=1) + spfh
+    fpfh[~has] = 0.0
+    return fpfh
+
+
+def feature_correspondences(src_feat, tgt_feat, mutual=True, ransac_n=3):
+    """Nearest target feature of every source feature (exact, ties to the lower index), and with
+    the mutual filter only the pairs that are each other's nearest -- unless fewer than
+    3 * ransac_n survive, then all of them (RegistrationRANSACBasedOnFeatureMatching)."""
+    a = np.asarray(src_feat, dtype=np.float64)
+    b = np.asarray(tgt_feat, dtype=np.float64)
+    ij = _feature_nn(a, b)
+    corr = np.stack([np.arange(len(a)), ij], axis=1)
+    if mutual:
+        ji = _feature_nn(b, a)
+        m = ji[ij] == np.arange(len(a))
+        if m.sum() >= 3 * ransac_n:
+            corr = corr[m]
+    return corr
+
+
+def _feature_nn(a, b, chunk=1024):
+    out = np.empty(len(a), np.int64)
+    bb = (b * b).sum(axis=1)
+    for s in range(0, len(a), chunk):
+        q = a[s:s + chunk]
+        d2 = ((q[:, None, :] - b[None, :, :]) ** 2).sum(axis=2)
+        out[s:s + chunk] = np.argmin(d2, axis=1)      # first minimum: lowest index on ties
+        del d2
+    del bb
+    return out
+
+
+def ransac_samples(seed, n_corr, iters, ransac_n=3):
+    """ransac_n correspondence indices per iteration, with replacement (Open3D draws each with a
+    uniform integer generator): splitmix64(seed) streams, value % n_corr."""
+    seed &= _M64
+    out = np.zeros((iters, ransac_n), np.int64)
+    for it in range(iters):
+        for j in range(ransac_n):
+            out[it, j] = _splitmix(seed, ransac_n * it + j) % n_corr
+    return out
+
+
+def ransac_feature_matching(source, target, corres, max_corr=5.0, edge=0.9, max_iteration=100000,
+                            confidence=0.999, seed=0, ransac_n=3):
+    """RegistrationRANSACBasedOnCorrespondence, sequential: per iteration below the running
+    estimate k, sample, Umeyama, edge-length + distance checks, evaluate (1-NN within max_corr);
+    better = higher fitness, then lower rmse; a better result sets
+    k = ceil(log(1 - confidence) / log(1 - r^ransac_n)) from its correspondence inlier ratio r.
+    Returns dict(transformation, fitness, inlier_rmse, evaluated)."""
+    src = np.asarray(source, dtype=np.float64)
+    tgt = np.asarray(target, dtype=np.float64)
+    corres = np.asarray(corres, dtype=np.int64)
+    tree = cKDTree(tgt)
+    best = dict(transformation=np.eye(4), fitness=0.0, inlier_rmse=0.0, evaluated=0)
+    if len(corres) < ransac_n:
+        return best
+    est_k = max_iteration
+    samples = ransac_samples(seed, len(corres), max_iteration, ransac_n)
+    cs, ct = src[corres[:, 0]], tgt[corres[:, 1]]
+    for it in range(max_iteration):
+        if it >= est_k:
+            break
+        c = corres[samples[it]]
+        ps, pt = src[c[:, 0]], tgt[c[:, 1]]
+        T = umeyama(ps, pt)
+        ok = True
+        for i in range(ransac_n):
+            for j in range(i + 1, ransac_n):
+                ds = math.sqrt(_dot(ps[i] - ps[j], ps[i] - ps[j]))
+                dt = math.sqrt(_dot(pt[i] - pt[j], pt[i] - pt[j]))
+                if ds < dt * edge or dt < ds * edge:
+                    ok = False
+        if ok:
+            q = transform_points(T, ps)
+            ok = bool(np.all(np.sqrt(_dot(pt - q, pt - q)) <= max_corr))
+        if not ok:
+            continue
+        best["evaluated"] += 1
+        q = transform_points(T, src)
+        _, _, fit, rmse = correspond(tree, tgt, q, max_corr)
+        if fit > best["fitness"] or (fit == best["fitness"] and rmse < best["inlier_rmse"]):
+            best.update(transformation=T, fitness=fit, inlier_rmse=rmse)
+            qc = transform_points(T, cs)
+            ratio = float(np.mean(_dot(qc - ct, qc - ct) < max_corr * max_corr))
+            if ratio > 0.0:
+                k = math.log(1.0 - confidence) / math.log(1.0 - ratio ** ransac_n) if ratio < 1.0 else 0.0
+                if k < est_k:
+                    est_k = int(math.ceil(k))
+    return best
+
+
+def preprocess_fpfh(points_raw, seed=0):
+    """KeyFrame.preprocess_fpfh (keyframe.py:191-229) for voxel_size None: filter, normals
+    (r 0.3, max_nn 300), ground plane + split, normals of both parts oriented to the first ones
+    (r 0.5 ground, 0.3 rest), FPFH of the non-ground part (r 0.3, max_nn 100)."""
+    P = filter_radius_height(points_raw)
+    N = estimate_normals(P)
+    plane = calculate_plane(P, seed=seed)
+    a, b, c, d = plane
+    dist = np.abs(a * P[:, 0] + b * P[:, 1] + c * P[:, 2] + d) / np.sqrt(a * a + b * b + c * c)
+    m = dist < 0.4
+    g, ng = P[m], P[~m]
+    gn = estimate_normals_oriented(g, N[m], 0.5, 300)
+    ngn = estimate_normals_oriented(ng, N[~m], 0.3, 300)
+    return dict(points=P, normals=N, plane=plane, ground=g, ground_normals=gn, rest=ng,
+                rest_normals=ngn, fpfh=compute_fpfh(ng, ngn, 0.3, 100))
+
+
+def global_registration(src, tgt, seed=0, fpfh_threshold=5.0, max_corr=DISTANCE_THRESHOLD):
+    """KeyFrame.global_registration: RANSAC on the non-ground parts' FPFH matches, then P2Plane
+    ICP of the filtered clouds from the RANSAC result (src / tgt: preprocess_fpfh dicts)."""
+    corres = feature_correspondences(src["fpfh"], tgt["fpfh"], mutual=True)
+    r = ransac_feature_matching(src["rest"], tgt["rest"], corres, fpfh_threshold, seed=seed)
+    icp = registration_icp(src["points"], tgt["points"], max_corr, r["transformation"], "p2plane",
+                           tgt["normals"])
+    return icp, r, corres

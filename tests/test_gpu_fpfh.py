@@ -1,0 +1,74 @@
+"""GPU: the 'fpfh' method -- oriented part normals, FPFH features, feature
+matches with the mutual filter, the feature RANSAC and the P2Plane refinement -- against the
+oracle (oracle/open3d_restated.py). The reference's own RANSAC uses Open3D's unseeded RNG (its
+result changes run to run); here both sides draw the same splitmix64(seed) samples, so they take
+the same hypotheses whenever their feature matches agree."""
+import numpy as np
+import pytest
+
+from lidar_slam_arvc_amd import datasets, se3, synthetic
+from lidar_slam_arvc_amd.keyframemanager import KeyFrameManager
+from oracle import open3d_restated as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fpfh_pair(tmp_path_factory):
+    seq = synthetic.make_sequence(2, seed=3, model=synthetic.HDL64)
+    d = str(tmp_path_factory.mktemp("fpfh"))
+    times = datasets.write_euroc(d, seq)
+    kfm = KeyFrameManager(d, np.array(times), voxel_size=None, method="fpfh")
+    for i in range(2):
+        kfm.add_keyframe(i)
+        kfm.load_pointcloud(i)
+        kfm.pre_process(i)
+    ref = [O.preprocess_fpfh(s) for s in seq.scans]
+    yield seq, kfm, ref
+    for i in range(2):
+        kfm.unload_pointcloud(i)
+
+
+def test_fpfh_parts_and_features(fpfh_pair):
+    seq, kfm, ref = fpfh_pair
+    for kf, r in zip(kfm.keyframes, ref):
+        ng = kf.pointcloud_non_ground_plane
+        assert np.array_equal(ng.points, r["rest"])
+        # oriented to the first normals: same sign as the oracle, not just the same line
+        dots = np.sum(ng.normals * r["rest_normals"], axis=1)
+        assert np.mean(dots > 1 - 1e-5) > 0.999
+        F = kf.pointcloud_fpfh.data.T
+        assert F.shape == r["fpfh"].shape
+        close = np.all(np.abs(F - r["fpfh"]) < 1e-6 * (1 + np.abs(r["fpfh"])), axis=1)
+        assert close.mean() > 0.99                   # pair-feature bin edges may differ rarely
+
+
+def test_feature_matches_and_global_registration(fpfh_pair):
+    seq, kfm, ref = fpfh_pair
+    dev = kfm._dev
+    kt, ks = kfm.keyframes
+    corres = dev.feature_correspondences(ks._planes[1], kt._planes[1], mutual=True)
+    rc = O.feature_correspondences(ref[1]["fpfh"], ref[0]["fpfh"], mutual=True)
+    a = {tuple(x) for x in corres.tolist()}
+    b = {tuple(x) for x in rc.tolist()}
+    assert len(a ^ b) <= max(2, len(b) // 100)
+    T = kfm.compute_transformation(0, 1, se3.HomogeneousMatrix(np.eye(4)))
+    icp, r, _ = O.global_registration(ref[1], ref[0])
+    if a == b:                                        # same matches -> same hypotheses
+        assert kt.last_ransac["evaluated"] == r["evaluated"]
+        assert np.abs(kt.last_ransac["transformation"] - r["transformation"]).max() < 1e-6
+    assert np.abs(T.array[:3, :3] - icp["transformation"][:3, :3]).max() < 1e-4
+    assert np.abs(T.array[:3, 3] - icp["transformation"][:3, 3]).max() < 1e-3
+
+
+def test_ransac_seeded_and_errors(fpfh_pair):
+    seq, kfm, ref = fpfh_pair
+    dev = kfm._dev
+    kt, ks = kfm.keyframes
+    corres = dev.feature_correspondences(ks._planes[1], kt._planes[1])
+    r1 = dev.ransac_feature(ks._planes[1], kt._planes[1], corres, seed=5)
+    r2 = dev.ransac_feature(ks._planes[1], kt._planes[1], corres, seed=5)
+    assert np.array_equal(r1["transformation"], r2["transformation"])
+    assert r1["fitness"] == r2["fitness"] and r1["evaluated"] == r2["evaluated"]
+    with pytest.raises(RuntimeError, match="out of range"):
+        dev.ransac_feature(ks._planes[1], kt._planes[1], np.array([[10**7, 0]] * 4))
