@@ -208,7 +208,7 @@ def main():
         achieved = nn["algo_bytes"] / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "nn_traffic.json")
-        if os.path.exists(tfile) and not ouster:
+        if os.path.exists(tfile) and not (ouster or loop):
             with open(tfile) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
