@@ -18,6 +18,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import threading
 import sys
 import time
 
@@ -45,6 +46,10 @@ def parse():
                     help="0: 256 (hdl64), 32 (ouster), 512 (loop_closure)")
     ap.add_argument("--seed", type=int, default=-1, help="-1: 3 (hdl64), 5 (ouster)")
     ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
+    ap.add_argument("--streams", type=int, default=1,
+                    help="hdl64_seq: independent contexts (HIP streams) per GPU, each registering a "
+                         "contiguous run of the pairs from its own host thread, so one run's "
+                         "latency-bound ICP passes overlap another's normal estimation")
     ap.add_argument("--cpu-sample-pairs", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -124,6 +129,8 @@ def main():
     from lidar_slam_arvc_amd import _lib, synthetic
     from lidar_slam_arvc_amd.distributed import compose_global_sharded
 
+    extra_ids = []                                   # (context, handle) of extra runs
+    devs = [None]
     ouster = args.workload == "ouster_multiscale"
     loop = args.workload == "loop_closure"
     P = args.pairs_per_gpu or (32 if ouster else (512 if loop else 256))
@@ -170,18 +177,43 @@ def main():
     else:
         prep = _lib.prep_params(want_normals=want_normals, grid_cell=args.grid_cell)
         icp = _lib.icp_params(method=args.method)
+        S = max(1, min(args.streams, P))
+        cut = [round(k * P / S) for k in range(S + 1)]          # pair runs [cut[s], cut[s+1])
+        devs = [dev] + [_lib.Device(local) for _ in range(S - 1)]
+        # run s owns keyframes cut[s] .. cut[s+1] (the shared end keyframe is in both runs)
+        run_ids = [ids[cut[0]:cut[1] + 1]] + [[devs[k].upload(seq.scans[j])
+                                                for j in range(cut[k], cut[k + 1] + 1)]
+                                               for k in range(1, S)]
+        extra_ids.extend((devs[k], h) for k in range(1, S) for h in run_ids[k])
+
+        def run(k, out):
+            d, hs = devs[k], run_ids[k]
+            n = d.preprocess(hs, prep)
+            out[k] = (n if k == 0 else n[1:], d.icp_batch(hs[1:], hs[:-1],
+                                                          seq.priors[cut[k]:cut[k + 1]], icp))
 
         def step():
-            n = dev.preprocess(ids, prep)
-            res = dev.icp_batch(ids[1:], ids[:-1], seq.priors, icp)
+            out = [None] * S
+            th = [threading.Thread(target=run, args=(k, out)) for k in range(1, S)]
+            for t in th:
+                t.start()
+            run(0, out)
+            for t in th:
+                t.join()
+            if any(o is None for o in out):
+                raise RuntimeError("a registration run failed")
+            n = np.concatenate([o[0] for o in out])
+            res = [r for o in out for r in o[1]]
             rel = np.stack([r["transformation"] for r in res])
             compose_global_sharded(rel, group=group, device=cuda)
             return n, res
 
     for _ in range(args.warmup):
         step()
-    dev.reset_stats()
-    dev.set_timing(True)
+    devs = [d for d in devs if d is not None] or [dev]
+    for d in devs:
+        d.reset_stats()
+        d.set_timing(True)
     if group is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -193,14 +225,23 @@ def main():
     if group is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dev.set_timing(False)
+    for d in devs:
+        d.set_timing(False)
     if group is not None:
         t = torch.tensor([dt], dtype=torch.float64, device=cuda)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    stats = {k: dev.kernel_stats(k) for k in KERNELS}
-    nn = dev.kernel_stats("nn_pass")   # check + search + fallback of every ICP pass
+    def kstats(name):   # summed over the contexts (their kernels may overlap in time)
+        tot = {"launches": 0, "ms": 0.0, "algo_bytes": 0.0}
+        for d in devs:
+            st = d.kernel_stats(name)
+            for key in tot:
+                tot[key] += st[key]
+        return tot
+
+    stats = {k: kstats(k) for k in KERNELS}
+    nn = kstats("nn_pass")   # check + search + fallback of every ICP pass
     n_pts, res = last
     iters = [r["iterations"] for r in res]
     out = None
@@ -264,6 +305,7 @@ def main():
                        if loop else
                        {"workload": f"hdl64_64k_{args.method}_seq",
                         "pairs_per_gpu": P, "global_pairs": world * P,
+                        "streams_per_gpu": max(1, min(args.streams, P)),
                         "points_per_scan_post_filter": int(np.mean(n_pts)),
                         "rays_per_scan": 65536, "method": args.method,
                         "max_correspondence_distance": 10.0,
@@ -274,14 +316,14 @@ def main():
             "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
                                       for k, v in stats.items() if v["launches"]},
             "nn_uncertified_fraction_after_pass0": round(
-                dev.kernel_stats("nn_uncertified")["launches"] /
-                max(dev.kernel_stats("nn_queries")["launches"] -
-                    dev.kernel_stats("nn_queries_first_pass")["launches"], 1), 5),
+                kstats("nn_uncertified")["launches"] /
+                max(kstats("nn_queries")["launches"] -
+                    kstats("nn_queries_first_pass")["launches"], 1), 5),
             "nn_fallback_fraction": {
-                "all_passes": round(dev.kernel_stats("nn_pending")["launches"] /
-                                    max(dev.kernel_stats("nn_queries")["launches"], 1), 5),
-                "first_pass": round(dev.kernel_stats("nn_pending_first_pass")["launches"] /
-                                    max(dev.kernel_stats("nn_queries_first_pass")["launches"], 1), 5)}
+                "all_passes": round(kstats("nn_pending")["launches"] /
+                                    max(kstats("nn_queries")["launches"], 1), 5),
+                "first_pass": round(kstats("nn_pending_first_pass")["launches"] /
+                                    max(kstats("nn_queries_first_pass")["launches"], 1), 5)}
         }
         print(json.dumps(out), flush=True)
     if group is not None:
@@ -291,6 +333,8 @@ def main():
         ms.release()
     for i in ids:
         dev.release(i)
+    for d, h in extra_ids:
+        d.release(h)
 
 
 if __name__ == "__main__":
