@@ -378,6 +378,7 @@ struct NormalParams {
     float r2_hi;      // f32 d^2 above this: certainly outside
     float hscale;     // f32 of the level-0 histogram scale NB8 / r^2 (see normals_kernel)
     int max_nn;
+    int dense_cell;   // own cell holds >= this many points: predicted > max_nn neighbours (0: off)
 };
 
 // Offsets of a candidate from the query in f64 (exact: both are f32 values) with their squares,
@@ -524,8 +525,9 @@ __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, fl
 // window. Long runs find the window's first point by binary search on x (a run averages ~140
 // points of which ~30 lie left of the window on HDL-64 scans); the walk stops past xh.
 constexpr uint32_t SCAN_BSEARCH = 16;
+constexpr int NORMALS_G_DEFAULT = 4;
 
-template <typename Body>
+template <int G, typename Body>
 __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float xl, float xh,
                                          Body &&body) {
     if (b - a > SCAN_BSEARCH) {
@@ -539,12 +541,30 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
         a = lo;
     }
     if (a >= b) return;
-    float4 p = lsm_ld(xyz, a);
-    for (uint32_t k = a; k < b; ++k) {
-        const float4 pn = lsm_ld(xyz, min(k + 1, b - 1));   // next point in flight meanwhile
-        if (p.x > xh) break;
-        if (p.x >= xl) body(p, k);
-        p = pn;
+    if (G == 1) {
+        float4 p = lsm_ld(xyz, a);
+        for (uint32_t k = a; k < b; ++k) {
+            const float4 pn = lsm_ld(xyz, min(k + 1, b - 1));   // next point in flight meanwhile
+            if (p.x > xh) break;
+            if (p.x >= xl) body(p, k);
+            p = pn;
+        }
+        return;
+    }
+    // G points per memory round trip: the walk is a chain of L2 hits, one latency each
+    for (uint32_t k = a; k < b; k += G) {
+        float4 p[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) p[g] = lsm_ld(xyz, min(k + uint32_t(g), b - 1));
+        bool stop = false;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            if (!stop) {
+                if (k + uint32_t(g) >= b || p[g].x > xh) stop = true;
+                else if (p[g].x >= xl) body(p[g], k + uint32_t(g));
+            }
+        }
+        if (stop) break;
     }
 }
 
@@ -603,6 +623,11 @@ __device__ __forceinline__ int sel_classify(const Sel &S, double d2, uint32_t k)
     return b < S.b ? -1 : (b > S.b ? 1 : 0);
 }
 
+// fire-and-forget LDS add (ds_add_u32: no read-back, so the walk does not wait on LDS)
+__device__ __forceinline__ void lds_add(uint32_t *a, uint32_t v) {
+    __hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Accumulator policies of hybrid_lane: what is done with the neighbourhood of a point.
 //   add(p, k): neighbour k (sorted index) at p; reset(): drop everything added; finish(): the
 //   neighbourhood is complete.
@@ -638,7 +663,7 @@ struct ListAcc {
 
 // KDTreeSearchParamHybrid(radius, max_nn) neighbourhood of point j of cloud C by one lane (H: the
 // lane's HSTRIDE-word LDS row), handed to `acc`.
-template <typename Acc>
+template <int G, typename Acc>
 __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                             unsigned long long *stats, uint32_t *H, Acc &acc) {
     uint8_t *H8 = reinterpret_cast<uint8_t *>(H);
@@ -649,13 +674,27 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
     bool sat = false;
     int count = 0;
+    // Density prediction: a point whose own cell is crowded almost always has more than max_nn
+    // ball neighbours, and then scan 1's neighbourhood would be dropped again. Such points skip
+    // acc.add in scan 1 (histogram only); a wrong guess costs one plain rescan below, which
+    // visits the ball in scan 1's order (identical sums).
+    bool dense = false;
+    if (np.dense_cell > 0) {
+        auto cc = [](float v, float o, float inv, int n) {
+            const int c = (int)floorf((v - o) * inv);
+            return c < 0 ? 0 : (c > n - 1 ? n - 1 : c);
+        };
+        const int l = lsm_cell_lin(C.nbx, C.nby, cc(qf.x, C.ox, C.inv_cell, C.nx),
+                                   cc(qf.y, C.oy, C.inv_cell, C.ny), cc(qf.z, C.oz, C.inv_cell, C.nz));
+        dense = int(lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l)) >= np.dense_cell;
+    }
     // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
     // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
     // f32 d^2 and the scale are within 4.2e-7 relative, t < 128). The rest (the sphere's
     // rounding band, bin edges) take the exact f64 distance, so the histogram is the one the
     // f64 binning of the later scans implies.
     ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+        scan_run<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
             const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
             const float f = dx * dx + dy * dy + dz * dz;
             const float t = f * np.hscale;
@@ -668,21 +707,36 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                 if (o.d2 < np.r2) bb = sel_level_bin(S, o.d2, k);
             }
             if (bb >= 0) {
-                acc.add(p, k);
+                if (!dense) acc.add(p, k);
                 ++count;
-                const uint32_t v = H8[bb];
-                sat |= v == 255u;
-                H8[bb] = uint8_t(v + (v < 255u ? 1u : 0u));
+                lds_add(H + (bb >> 2), 1u << ((bb & 3) << 3));   // u8 bin, carries detected below
             }
         });
     });
-    if (count <= np.max_nn) {
-        acc.finish();
-        return;
-    }
-    acc.reset();
-    if (stats) atomicAdd(stats, 1ull);   // points that needed the kNN truncation
     double top = np.r2;   // every point below or member has d2 <= top (up to rounding)
+    uint32_t need = uint32_t(np.max_nn);   // still to take from the members
+    if (count <= np.max_nn) {
+        if (!dense) {
+            acc.finish();
+            return;
+        }
+        S.dlo = INFINITY;   // mispredicted: every ball point is below, the final pass adds them
+        need = 0;
+    } else {
+        if (!dense) acc.reset();
+        if (stats) atomicAdd(stats, 1ull);   // points that needed the kNN truncation
+        // A u8 bin that passed 255 carried into its neighbour byte (or out of its word): each
+        // such carry lowers the bin total by 255 or 256, so the total tells.
+        if (count > 255) {
+            uint32_t tot = 0;
+#pragma unroll
+            for (int b = 0; b < NB8 / 4; ++b) {
+                const uint32_t w = H[b];
+                tot += (w & 0xffu) + ((w >> 8) & 0xffu) + ((w >> 16) & 0xffu) + (w >> 24);
+            }
+            sat = tot != uint32_t(count);
+        }
+    }
     // rescan the members of the current state: their key extremes and a histogram by `next`
     auto refine = [&](const Sel &next, double &dmin, double &dmax, uint32_t &kmin, uint32_t &kmax) {
 #pragma unroll
@@ -692,10 +746,10 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         kmin = 0xffffffffu;
         kmax = 0u;
         ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
-            scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+            scan_run<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
                 Off o;
                 if (in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
-                    H[sel_level_bin(next, o.d2, k)] += 1;
+                    lds_add(H + sel_level_bin(next, o.d2, k), 1u);
                     dmin = fmin(dmin, o.d2);
                     dmax = fmax(dmax, o.d2);
                     kmin = min(kmin, k);
@@ -704,9 +758,8 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
             });
         });
     };
-    uint32_t need = uint32_t(np.max_nn);   // still to take from the members
     bool u8 = true;
-    if (sat) {                             // a u8 bin saturated: level 0 as 32 x u32 bins
+    if (count > np.max_nn && sat) {                             // a u8 bin saturated: level 0 as 32 x u32 bins
         Sel next = S;
         next.scale = double(NB32) / np.r2;
         next.nb = NB32;
@@ -719,7 +772,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         S = next;
         u8 = false;
     }
-    for (int it = 0; it < MAX_REFINE; ++it) {
+    for (int it = 0; it < MAX_REFINE && count > np.max_nn; ++it) {
         uint32_t acc = 0;
         int bstar = S.nb - 1;
         for (int b = 0; b < S.nb; ++b) {
@@ -769,7 +822,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // final pass: everything below, plus the `need` smallest members
     uint32_t m = 0;
     ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+        scan_run<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
             const float fd = f32_d2(qf, p);
             if (fd > np.r2_hi) return;
             const Off o = make_off(p, qx, qy, qz);
@@ -803,6 +856,20 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     acc.finish();
 }
 
+// Own-cell population from which a point is predicted to have more than max_nn neighbours in
+// its ball (a performance guess only: both outcomes are exact). On HDL-64 scans with 0.3 m cells
+// and max_nn = 300, 80 points mispredict ~4 % of the ball work either way.
+// LSM_NORMALS_DENSE=<fraction of max_nn> overrides 0.27; 0 turns the prediction off.
+int dense_cell_threshold(int max_nn) {
+    static const double frac = [] {
+        const char *e = getenv("LSM_NORMALS_DENSE");
+        return e ? atof(e) : 0.27;
+    }();
+    if (frac <= 0.0) return 0;
+    return std::max(1, int(std::lround(frac * double(max_nn))));
+}
+
+template <int G>
 __global__ void __launch_bounds__(PT_THREADS)
 normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
                unsigned long long *stats) {
@@ -814,7 +881,7 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     const float4 q = lsm_ld(C.xyz, j);
     CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
-    hybrid_lane(C, j, np, stats, lds + threadIdx.x * HSTRIDE, acc);
+    hybrid_lane<G>(C, j, np, stats, lds + threadIdx.x * HSTRIDE, acc);
 }
 
 // Neighbour lists of FPFH (ComputeFPFHFeature's KDTreeSearchParamHybrid): at most `cap` per
@@ -830,7 +897,7 @@ nbr_lists_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, int32_t *
     const float4 q = lsm_ld(C.xyz, j);
     ListAcc acc{idx + size_t(j) * cap, d2 + size_t(j) * cap, count + j, cap, 0,
                 double(q.x), double(q.y), double(q.z)};
-    hybrid_lane(C, j, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
+    hybrid_lane<NORMALS_G_DEFAULT>(C, j, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1290,6 +1357,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         np.r2_hi = float(np.r2 * (1.0 + 4e-6));
         np.hscale = float(double(NB8) / np.r2);
         np.max_nn = p.max_nn;
+        np.dense_cell = dense_cell_threshold(p.max_nn);
         ctx->tic("normals", &ev);
         {
             static const bool nstats = getenv("LSM_NORMALS_STATS") != nullptr;
@@ -1298,7 +1366,15 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 d_ns = (unsigned long long *)ctx->buf("n_stats", 8 * 8);
                 LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 64, st));
             }
-            normals_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
+            static const int G = [] {   // LSM_NORMALS_G: points per load group of the walks
+                const char *e = getenv("LSM_NORMALS_G");
+                return e ? atoi(e) : NORMALS_G_DEFAULT;
+            }();
+            const dim3 ng(unsigned(psegs.size()));
+            if (G == 1) normals_kernel<1><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
+            else if (G == 2) normals_kernel<2><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
+            else if (G == 8) normals_kernel<8><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
+            else normals_kernel<4><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
             if (nstats) {
                 unsigned long long h = 0;
                 LSM_HIP_TRY(ctx, hipMemcpyAsync(&h, d_ns, 8, hipMemcpyDeviceToHost, st));
@@ -1572,6 +1648,7 @@ int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn) {
     np.r2_hi = float(np.r2 * (1.0 + 4e-6));
     np.hscale = float(double(NB8) / np.r2);
     np.max_nn = max_nn;
+    np.dense_cell = dense_cell_threshold(max_nn);
     hipEvent_t ev;
     ctx->tic("fpfh", &ev);
     nbr_lists_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_idx, d_d2, d_cnt,
