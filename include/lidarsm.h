@@ -53,7 +53,7 @@ typedef struct {
     double normal_radius;  /* 0.3                                          */
     int32_t max_nn;        /* 300                                          */
     int32_t want_normals;  /* 1 for 'icppointplane', 0 for 'icppointpoint' */
-    double grid_cell;      /* spatial-hash cell edge in metres; <= 0 -> library default */
+    double grid_cell;      /* spatial-hash cell edge in metres; <= 0 -> library default (0.375) */
 } lsm_prep_params;
 
 /* registration_icp(source, target, max_correspondence_distance, init, estimation, criteria)

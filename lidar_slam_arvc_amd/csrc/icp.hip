@@ -43,6 +43,10 @@ struct NNParams {
     int method;
     int max_iter;
     double rel_fit, rel_rmse;
+    int split_max;     // most lanes one uncertified query's box search is split over
+    float m0;          // rho margin of the searches without a previous pass (see prune2)
+    uint32_t lin;      // runs of at most this many points are scanned whole (no entry search)
+    double m_mul, m_add;   // rho margin of a search after a pass that moved the query by dq
 };
 
 // Correspondence state of one source point, carried from pass to pass (SoA arrays):
@@ -122,33 +126,87 @@ __device__ __forceinline__ float sqd(const float4 t, float qx, float qy, float q
 // from the query: enter at the query's x (binary search on long runs) and walk outwards while
 // dx^2 + dyz2 <= the pruning radius (strict '>' stops: equal distances are still examined, so
 // (d2, index) ties resolve exactly as a full scan would).
-constexpr uint32_t NN_LINEAR = 8;
+
+// Search statistics (LSM_NN_STATS=1, diagnostics only): per lane, reduced per wave at the end.
+struct NNStat {
+    uint32_t v[8];   // searched, rows, runs, bsearch steps, points, sum K, cold, pending
+};
+constexpr int NN_NSTAT = 8;
+#define NN_ST(ns, c, x) \
+    do {                \
+        if (ns) (ns)->v[c] += (x); \
+    } while (0)
+
+// Loads are issued NN_G at a time (independent addresses: one memory round trip per group rather
+// than per point); a group may read up to NN_G - 1 points past the walk's stop, never past the
+// run. Short runs (<= lin points) are scanned whole.
+#ifndef LSM_NN_G
+#define LSM_NN_G 4
+#endif
+constexpr int NN_G = LSM_NN_G;
 
 __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float qx,
-                                         float qy, float qz, float dyz2, Top2 &t2) {
-    if (b - a <= NN_LINEAR) {
-        for (uint32_t k = a; k < b; ++k) top2_add(sqd(lsm_ld(xyz, k), qx, qy, qz), int(k), t2);
+                                         float qy, float qz, float dyz2, Top2 &t2, uint32_t lin,
+                                         NNStat *ns = nullptr) {
+    NN_ST(ns, 2, 1);
+    if (b - a <= lin) {
+        NN_ST(ns, 4, b - a);
+        for (uint32_t k = a; k < b; k += NN_G) {
+            float4 t[NN_G];
+#pragma unroll
+            for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, min(k + uint32_t(g), b - 1));
+#pragma unroll
+            for (int g = 0; g < NN_G; ++g)
+                if (k + uint32_t(g) < b) top2_add(sqd(t[g], qx, qy, qz), int(k + uint32_t(g)), t2);
+        }
         return;
     }
     const float *xs = reinterpret_cast<const float *>(xyz);
     uint32_t lo = a, hi = b;
     while (lo < hi) {
+        NN_ST(ns, 3, 1);
         const uint32_t mid = (lo + hi) >> 1;
         if (lsm_ld(xs, size_t(mid) * 4) < qx) lo = mid + 1;
         else hi = mid;
     }
-    for (uint32_t k = lo; k < b; ++k) {
-        const float4 t = lsm_ld(xyz, k);
-        const float dx = t.x - qx;
-        if (dx * dx + dyz2 > t2.lim) break;
-        top2_add(sqd(t, qx, qy, qz), int(k), t2);
+    // rightwards from lo (x >= qx), then leftwards from lo - 1 (x < qx)
+    for (uint32_t k = lo; k < b; k += NN_G) {
+        float4 t[NN_G];
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, min(k + uint32_t(g), b - 1));
+        bool stop = false;
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) {
+            if (!stop) {
+                const float dx = t[g].x - qx;
+                if (k + uint32_t(g) >= b || dx * dx + dyz2 > t2.lim) {
+                    stop = true;
+                } else {
+                    NN_ST(ns, 4, 1);
+                    top2_add(sqd(t[g], qx, qy, qz), int(k + uint32_t(g)), t2);
+                }
+            }
+        }
+        if (stop) break;
     }
-    for (uint32_t k = lo; k > a;) {
-        --k;
-        const float4 t = lsm_ld(xyz, k);
-        const float dx = qx - t.x;
-        if (dx * dx + dyz2 > t2.lim) break;
-        top2_add(sqd(t, qx, qy, qz), int(k), t2);
+    for (int k = int(lo) - 1; k >= int(a); k -= NN_G) {
+        float4 t[NN_G];
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, uint32_t(max(k - g, int(a))));
+        bool stop = false;
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) {
+            if (!stop) {
+                const float dx = qx - t[g].x;
+                if (k - g < int(a) || dx * dx + dyz2 > t2.lim) {
+                    stop = true;
+                } else {
+                    NN_ST(ns, 4, 1);
+                    top2_add(sqd(t[g], qx, qy, qz), k - g, t2);
+                }
+            }
+        }
+        if (stop) break;
     }
 }
 
@@ -258,9 +316,41 @@ constexpr int NN_KCOLD = 2;   // cold start (no previous neighbour): 5x5x5 cells
 
 // Returns true when resolved (result / rho set), false when the fallback must finish it (t2
 // holds what the box search found).
+// (nearest, second) reduction over the L lanes of a query group (L a power of two, the group
+// aligned inside the wave); lanes holding the same point merge their second distances.
+// `lim` becomes a valid pruning bound of the whole group: every point some lane skipped is at
+// least that lane's lim away, every examined non-best point at least the merged second.
+__device__ __forceinline__ void group_top2(Top2 &t, int L) {
+    float lim = t.lim;
+    for (int off = L >> 1; off > 0; off >>= 1) {
+        const float od = __shfl_xor(t.bd2, off, LSM_WAVE);
+        const int oi = __shfl_xor(t.bidx, off, LSM_WAVE);
+        const float os = __shfl_xor(t.sd2, off, LSM_WAVE);
+        lim = fminf(lim, __shfl_xor(lim, off, LSM_WAVE));
+        if (oi == t.bidx) {
+            t.sd2 = fminf(t.sd2, os);
+        } else if (better(od, oi, t.bd2, t.bidx)) {
+            t.sd2 = fminf(os, t.bd2);
+            t.bd2 = od;
+            t.bidx = oi;
+        } else {
+            t.sd2 = fminf(t.sd2, od);
+        }
+    }
+    t.lim = fminf(prune2(t.bd2, t.sd2, t.m), lim);
+}
+
+// Box search of one query by a group of L lanes (sub = this lane's index in the group): the
+// rows of the box are dealt round-robin over the group in centre-out order, each lane keeps
+// its own (nearest, second) and pruning radius, and the group merges them at the end. L = 1
+// is the plain per-lane search; a workgroup with few uncertified queries splits each over
+// several lanes, so a long search chain (a far or ambiguous query of a pair that keeps
+// iterating) is not left to one lane. Every lane of the group returns the same values.
 __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, const CloudDev &G,
                                          int i, int prev, float m, const NNParams &prm,
-                                         int &result, float &rho, Top2 &t2) {
+                                         int &result, float &rho, Top2 &t2, int sub = 0,
+                                         int L = 1, NNStat *ns = nullptr) {
+    NN_ST(ns, 0, 1);
     double qx64, qy64, qz64;
     transform_point(T, lsm_ld(S.xyz, i), qx64, qy64, qz64);
     const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
@@ -282,27 +372,32 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     if (t2.bd2 < INFINITY) {
         const float rc = sqrtf(t2.bd2) * G.inv_cell * 1.0001f + 1e-4f;
         K = rc >= float(NN_KMAX) ? NN_KMAX : max(1, (int)ceilf(rc));
+    } else {
+        NN_ST(ns, 6, 1);
     }
+    NN_ST(ns, 5, K);
     const int x0 = max(cx - K, 0), x1 = min(cx + K, G.nx - 1);
     const int y0 = max(cy - K, 0), y1 = min(cy + K, G.ny - 1);
     const int z0 = max(cz - K, 0), z1 = min(cz + K, G.nz - 1);
     const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
     const uint32_t *cs = G.cell_start;
+    const int W = 2 * K + 1;
 #pragma unroll 1
-    for (int iz = 0; iz <= 2 * K; ++iz) {
+    for (int iz = 0; iz < W; ++iz) {
         const int dz = (iz & 1) ? -((iz + 1) >> 1) : (iz >> 1);   // 0, -1, 1, -2, 2 ...
         const int z = cz + dz;
         if (z < z0 || z > z1) continue;
         const float wz = slab_cells2(fz, z) * c2;
         if (wz >= t2.lim) continue;
 #pragma unroll 1
-        for (int iy = 0; iy <= 2 * K; ++iy) {
+        for (int iy = (sub - iz * W) & (L - 1); iy < W; iy += L) {   // rows t == sub (mod L)
             const int dy = (iy & 1) ? -((iy + 1) >> 1) : (iy >> 1);
             const int y = cy + dy;
             if (y < y0 || y > y1) continue;
             const float wyz = wz + slab_cells2(fy, y) * c2;
             const float lim = t2.lim;
             if (wyz >= lim) continue;
+            NN_ST(ns, 1, 1);
             // cells of this row that can still hold a point within the pruning radius
             int xa = x0, xb = x1;
             if (lim < INFINITY) {
@@ -315,7 +410,7 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
                 const int xe = min(xb, x | (LSM_BLK - 1));   // end of this block's row part
                 const uint32_t a = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, x, y, z));
                 const uint32_t b = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, xe, y, z) + 1);
-                if (b > a) scan_run(G.xyz, a, b, qx, qy, qz, wyz, t2);
+                if (b > a) scan_run(G.xyz, a, b, qx, qy, qz, wyz, t2, prm.lin, ns);
                 x = xe + 1;
             }
         }
@@ -330,6 +425,8 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
                            cz + K + 1 < G.nz ? float(cz + K + 1) - fz : INFINITY);
     const float bound = fminf(bx, fminf(by, bz)) * G.cell;
     const float bound2 = bound * bound * 0.99999f;
+    if (L > 1) group_top2(t2, L);
+    if (!(t2.bd2 <= bound2 || bound >= prm.maxc)) NN_ST(ns, 7, sub == 0 ? 1 : 0);
     if (t2.bd2 <= bound2 || bound >= prm.maxc) {
         if (t2.bidx >= 0 && t2.bd2 < prm.maxc2) {
             result = t2.bidx;
@@ -382,7 +479,7 @@ __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &
                  ddz = double(qz) - double(float(zp));
     const double dq = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
     const double delta = dq * (1.0 + 1e-6) + 1e-7;
-    m = float(4.0 * dq + 1e-3);
+    m = float(prm.m_mul * dq + prm.m_add);
     const int prev = corr[g];
     const double r = double(rho[g]);
     if (prev >= 0) {
@@ -406,12 +503,23 @@ __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &
     return false;
 }
 
-template <bool CHECK>
+// per-wave sums of the lanes' statistics into stats[pass * NN_NSTAT + c]
+__device__ __forceinline__ void flush_stats(const NNStat &ls, unsigned long long *stats) {
+    for (int c = 0; c < NN_NSTAT; ++c) {
+        uint32_t v = ls.v[c];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, LSM_WAVE);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(stats + c, (unsigned long long)v);
+    }
+}
+
+template <bool CHECK, bool STATS = false>
 __global__ void __launch_bounds__(NN_THREADS)
 nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
           NNParams prm, int32_t *__restrict__ corr, float *__restrict__ rho,
           FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n, uint32_t queue_cap,
-          uint32_t *__restrict__ searched) {
+          uint32_t *__restrict__ searched, unsigned long long *__restrict__ stats = nullptr) {
+    NNStat ls{};
+    NNStat *ns = STATS ? &ls : nullptr;
     // one task per workgroup: the host sizes the grid from an earlier pass's plan, which only
     // shrinks, so waves may retire early (no barrier follows the compaction)
     BlockTask task;
@@ -422,7 +530,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
     const CloudDev G = cds[P.tgt];
     int i = task.start + threadIdx.x;
     bool live = i < S.n;
-    float m = 0.f;
+    float m = prm.m0;
     if (CHECK) {
         __shared__ int32_t s_idx[NN_THREADS];
         __shared__ float s_m[NN_THREADS];
@@ -446,24 +554,48 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         }
         __syncthreads();
         if (threadIdx.x == 0 && total > 0) atomicAdd(searched, uint32_t(total));
-        if (w * LSM_WAVE >= total) return;   // this wave has nothing to search
-        live = int(threadIdx.x) < total;
+        // few queries left: L lanes per query (power of two, at most split_max)
+        int L = 1;
+        while (L < prm.split_max && total * (2 * L) <= NN_THREADS) L *= 2;
+        const int q = int(threadIdx.x) / L;
+        if (w * LSM_WAVE >= total * L) return;   // this wave has nothing to search (no stats)
+        live = q < total;
         if (live) {
-            i = s_idx[threadIdx.x];
-            m = s_m[threadIdx.x];
+            i = s_idx[q];
+            m = s_m[q];
         }
+        const int sub = int(threadIdx.x) & (L - 1);
+        const int64_t g = P.src_off + i;
+        int result = -1;
+        float r = 0.f;
+        Top2 t2 = top2_init(-1, INFINITY, INFINITY, m);
+        bool pending = false;
+        if (live)
+            pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2, sub, L, ns);
+        const bool lead = live && sub == 0;
+        push_fallback(pending && lead, task.pair, i, m, t2, queue, queue_n, queue_cap);
+        if (lead) {
+            corr[g] = pending ? -2 : result;
+            rho[g] = r;
+        }
+        if (STATS) {
+            if (sub != 0) ls.v[0] = 0;   // one search per query
+            flush_stats(ls, stats);
+        }
+        return;
     }
     const int64_t g = P.src_off + i;
     int result = -1;
     float r = 0.f;
     Top2 t2 = top2_init(-1, INFINITY, INFINITY, m);
     bool pending = false;
-    if (live) pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2);
+    if (live) pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2, 0, 1, ns);
     push_fallback(pending, task.pair, i, m, t2, queue, queue_n, queue_cap);
     if (live) {
         corr[g] = pending ? -2 : result;
         rho[g] = r;
     }
+    if (STATS) flush_stats(ls, stats);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1018,6 +1150,25 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     prm.max_iter = max_iter;
     prm.rel_fit = p.relative_fitness;
     prm.rel_rmse = p.relative_rmse;
+    static const int SPLIT_MAX = [] {   // LSM_NN_SPLIT: 1 = one lane per query
+        const char *e = getenv("LSM_NN_SPLIT");
+        int v = e ? atoi(e) : 8;
+        int l = 1;
+        while (l * 2 <= v && l < 64) l *= 2;
+        return l;
+    }();
+    prm.split_max = SPLIT_MAX;
+    auto envf = [](const char *k, double d) {
+        const char *e = getenv(k);
+        return e ? atof(e) : d;
+    };
+    static const double M0 = envf("LSM_NN_M0", 0.0), MMUL = envf("LSM_NN_MMUL", 4.0),
+                        MADD = envf("LSM_NN_MADD", 1e-3);
+    prm.m0 = float(M0);
+    static const uint32_t LIN = uint32_t(envf("LSM_NN_LINEAR", 8));
+    prm.lin = LIN;
+    prm.m_mul = MMUL;
+    prm.m_add = MADD;
 
     // Passes are launched back to back; the plan of each pass is rebuilt on the device after the
     // solve (plan_kernel), and kernels past the plan's end exit at once. The host only polls,
@@ -1041,6 +1192,13 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     const bool nocert = nc_env && atoi(nc_env) != 0;
     double ms0 = 0.0;
     for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
+    static const bool nn_stats = getenv("LSM_NN_STATS") != nullptr;
+    unsigned long long *d_nst = nullptr;
+    if (nn_stats) {
+        d_nst = (unsigned long long *)ctx->buf("i_nnstats", size_t(ncnt) * NN_NSTAT * 8);
+        if (!d_nst) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_nst, 0, size_t(ncnt) * NN_NSTAT * 8, st));
+    }
     plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
     const TaskPlan tp{d_plan, d_pref, int(npairs)};
     int passes = 0, polled = 0;
@@ -1063,7 +1221,15 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         if (done) break;
         hipEvent_t ev;
         ctx->tic("nn", &ev);
-        if (pass == 0 || nocert)
+        if (d_nst) {
+            unsigned long long *sp = d_nst + size_t(pass) * NN_NSTAT;
+            if (pass == 0 || nocert)
+                nn_kernel<false, true><<<grid, NN_THREADS, 0, st>>>(
+                    tp, d_ps, d_cd, prm, d_corr, d_rho, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+            else
+                nn_kernel<true, true><<<grid, NN_THREADS, 0, st>>>(
+                    tp, d_ps, d_cd, prm, d_corr, d_rho, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+        } else if (pass == 0 || nocert)
             nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_rho, d_q,
                                                           d_qn + pass, qcap, d_sqn + pass);
         else
@@ -1098,6 +1264,18 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     }
     LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
     for (int k = 0; k < passes; ++k) ctx->event_pool.push_back(pass_ev[size_t(k)]);
+    if (d_nst) {   // per pass: searched, rows, runs, bsearch steps, points, K, cold, pending
+        std::vector<unsigned long long> h(size_t(passes) * NN_NSTAT);
+        LSM_HIP_TRY(ctx, hipMemcpy(h.data(), d_nst, h.size() * 8, hipMemcpyDeviceToHost));
+        for (int k = 0; k < passes; ++k) {
+            const unsigned long long *v = h.data() + size_t(k) * NN_NSTAT;
+            const double q = double(std::max(v[0], 1ull));
+            fprintf(stderr,
+                    "nnstat pass %2d: searched %9llu rows %.2f runs %.2f bsearch %.2f points %.2f "
+                    "K %.2f cold %.3f pending %.4f\n",
+                    k, v[0], v[1] / q, v[2] / q, v[3] / q, v[4] / q, v[5] / q, v[6] / q, v[7] / q);
+        }
+    }
     double nn_bytes = 0.0;
     {
         std::vector<double> hb(size_t(passes) + 1, 0.0);

@@ -31,6 +31,11 @@ constexpr int FILTER_PER_THREAD = 4;
 constexpr int FILTER_CHUNK = FILTER_THREADS * FILTER_PER_THREAD;
 constexpr int PT_THREADS = 256;
 constexpr int64_t MAX_CELLS_PER_CLOUD = int64_t(1) << 24;
+// Default cell edge of the keyframe grid (m). Measured on the HDL-64 bench (pairs/s):
+// 0.3 4136, 0.36 4308, 0.4 4336, 0.45 4177, 0.5 4028 -- larger cells cost the normals walk
+// (rows of 0.09+ m^2 cross-section) and the NN row walks, smaller ones push far queries into
+// the fallback (4x4x4-cell blocks shrink with the cell).
+constexpr float LSM_DEFAULT_GRID_CELL = 0.375f;
 
 struct Seg {           // (keyframe, first point) of one workgroup
     int32_t cloud;
@@ -378,7 +383,8 @@ struct NormalParams {
     float r2_hi;      // f32 d^2 above this: certainly outside
     float hscale;     // f32 of the level-0 histogram scale NB8 / r^2 (see normals_kernel)
     int max_nn;
-    int dense_cell;   // own cell holds >= this many points: predicted > max_nn neighbours (0: off)
+    float dense_k;    // own cell holds >= dense_k * cell^2 points: predicted > max_nn neighbours
+                      // (0: off)
 };
 
 // Offsets of a candidate from the query in f64 (exact: both are f32 values) with their squares,
@@ -679,14 +685,15 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // acc.add in scan 1 (histogram only); a wrong guess costs one plain rescan below, which
     // visits the ball in scan 1's order (identical sums).
     bool dense = false;
-    if (np.dense_cell > 0) {
+    if (np.dense_k > 0.f) {
         auto cc = [](float v, float o, float inv, int n) {
             const int c = (int)floorf((v - o) * inv);
             return c < 0 ? 0 : (c > n - 1 ? n - 1 : c);
         };
         const int l = lsm_cell_lin(C.nbx, C.nby, cc(qf.x, C.ox, C.inv_cell, C.nx),
                                    cc(qf.y, C.oy, C.inv_cell, C.ny), cc(qf.z, C.oz, C.inv_cell, C.nz));
-        dense = int(lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l)) >= np.dense_cell;
+        dense = float(lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l)) >=
+                np.dense_k * C.cell * C.cell;
     }
     // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
     // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
@@ -857,16 +864,17 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
 }
 
 // Own-cell population from which a point is predicted to have more than max_nn neighbours in
-// its ball (a performance guess only: both outcomes are exact). On HDL-64 scans with 0.3 m cells
-// and max_nn = 300, 80 points mispredict ~4 % of the ball work either way.
-// LSM_NORMALS_DENSE=<fraction of max_nn> overrides 0.27; 0 turns the prediction off.
-int dense_cell_threshold(int max_nn) {
+// its ball (a performance guess only: both outcomes are exact): frac * max_nn * (cell / r)^2,
+// a surface's share of the ball in one cell. On HDL-64 scans with cell = r = 0.3 m and
+// max_nn = 300, frac = 0.27 mispredicts ~4 % of the ball work either way.
+// LSM_NORMALS_DENSE=<frac> overrides 0.27; 0 turns the prediction off.
+float dense_k(int max_nn, double r2) {
     static const double frac = [] {
         const char *e = getenv("LSM_NORMALS_DENSE");
         return e ? atof(e) : 0.27;
     }();
-    if (frac <= 0.0) return 0;
-    return std::max(1, int(std::lround(frac * double(max_nn))));
+    if (frac <= 0.0 || r2 <= 0.0) return 0.f;
+    return float(frac * double(max_nn) / r2);
 }
 
 template <int G>
@@ -1226,7 +1234,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
 
     std::vector<GridGeo> geo(K);
     uint64_t cell_total = 0;
-    const float cell_req = p.grid_cell > 0 ? float(p.grid_cell) : 0.3f;
+    const float cell_req = p.grid_cell > 0 ? float(p.grid_cell) : LSM_DEFAULT_GRID_CELL;
     for (int k = 0; k < K; ++k) {
         GridGeo &G = geo[k];
         G.pt_off = woff[k];
@@ -1357,7 +1365,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         np.r2_hi = float(np.r2 * (1.0 + 4e-6));
         np.hscale = float(double(NB8) / np.r2);
         np.max_nn = p.max_nn;
-        np.dense_cell = dense_cell_threshold(p.max_nn);
+        np.dense_k = dense_k(p.max_nn, np.r2);
         ctx->tic("normals", &ev);
         {
             static const bool nstats = getenv("LSM_NORMALS_STATS") != nullptr;
@@ -1648,7 +1656,7 @@ int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn) {
     np.r2_hi = float(np.r2 * (1.0 + 4e-6));
     np.hscale = float(double(NB8) / np.r2);
     np.max_nn = max_nn;
-    np.dense_cell = dense_cell_threshold(max_nn);
+    np.dense_k = dense_k(max_nn, np.r2);
     hipEvent_t ev;
     ctx->tic("fpfh", &ev);
     nbr_lists_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_idx, d_d2, d_cnt,
