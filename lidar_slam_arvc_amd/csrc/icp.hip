@@ -626,6 +626,11 @@ __device__ __forceinline__ float gap2(float q, float lo, float hi) {
     return d * d;
 }
 
+// Blocks in Chebyshev ring r, and in the rings before r.
+__device__ __forceinline__ int ring_size(int r) { return r == 0 ? 1 : 24 * r * r + 2; }
+__device__ __forceinline__ int ring_prefix(int r) { return r == 0 ? 0 : (2 * r - 1) * (2 * r - 1) * (2 * r - 1); }
+constexpr int FB_R0 = 2;   // the fallback's first shell: rings 0 .. FB_R0 (5 x 5 x 5 blocks)
+
 // Chebyshev ring r of blocks around the origin block: t in [0, 24 r^2 + 2) -> offset.
 __device__ __forceinline__ void ring_offset(int r, int t, int &dx, int &dy, int &dz) {
     if (r == 0) {
@@ -663,10 +668,14 @@ __device__ __forceinline__ void ring_offset(int r, int t, int &dx, int &dy, int 
 __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
             const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
-            uint32_t queue_cap, int32_t *__restrict__ corr, float *__restrict__ rho) {
+            uint32_t queue_cap, int32_t *__restrict__ corr, float *__restrict__ rho,
+            unsigned long long *__restrict__ fstats = nullptr) {
     const int lane = threadIdx.x;
     const uint32_t total = min(*queue_n, queue_cap);
+    // statistics (LSM_NN_STATS): queries, rings, chunks, blocks scanned, points, hits, outside
+    uint32_t fs[7] = {0, 0, 0, 0, 0, 0, 0};
     for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
+        fs[0] += 1;
         const FallbackItem q = queue[it];
         const PairState &P = st[q.pair];
         const CloudDev S = cds[P.src];
@@ -684,6 +693,7 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
             fbound = INFINITY;
         } else if (box2 >= prm.maxc2) {
             fbound = sqrtf(box2);   // nothing within max_corr: every point is outside the box
+            fs[6] += 1;
         } else {
             const float invB = 1.f / B;
             const int qbx = (int)floorf((qx - G.ox) * invB), qby = (int)floorf((qy - G.oy) * invB),
@@ -691,14 +701,24 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
             auto outside = [](int v, int n) { return v < 0 ? -v : (v > n - 1 ? v - (n - 1) : 0); };
             const int r0 = max(outside(qbx, G.nbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
             const uint32_t *cs = G.cell_start;
-            for (int r = r0; r < 4096; ++r) {
-                const int nring = (r == 0) ? 1 : 24 * r * r + 2;
-                for (int base = 0; base < nring; base += LSM_WAVE) {
+            // shells of rings [ra, rb]: the first one (query inside the grid) covers rings
+            // 0 .. FB_R0 at once -- 125 blocks in two chunks, one merge and stop test -- and the
+            // rest are single rings. Lanes keep their own (nearest, second) across a shell's
+            // chunks (their pruning radii are only looser than the wave's); the shell ends with
+            // the wave merge and the stop test.
+            int ra = r0, rb = r0 == 0 ? FB_R0 : r0;
+            for (;;) {
+                fs[1] += 1;
+                const int nitems = ring_prefix(rb + 1) - ring_prefix(ra);
+                for (int base = 0; base < nitems; base += LSM_WAVE) {
+                    fs[2] += 1;
                     const int t = base + lane;
                     uint32_t a = 0, b = 0;
-                    if (t < nring) {
+                    if (t < nitems) {
+                        int r = ra, u = t;
+                        while (u >= ring_size(r)) u -= ring_size(r++);
                         int dx, dy, dz;
-                        ring_offset(r, t, dx, dy, dz);
+                        ring_offset(r, u, dx, dy, dz);
                         const int bx = qbx + dx, by = qby + dy, bz = qbz + dz;
                         if (bx >= 0 && bx < G.nbx && by >= 0 && by < G.nby && bz >= 0 &&
                             bz < G.nbz) {
@@ -716,13 +736,16 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
                     while (mask) {
                         const int src = __ffsll((unsigned long long)mask) - 1;
                         mask &= mask - 1;
-                        const uint32_t ra = __shfl(a, src, LSM_WAVE), rb = __shfl(b, src, LSM_WAVE);
-                        for (uint32_t k = ra + lane; k < rb; k += LSM_WAVE)
+                        const uint32_t ra_ = __shfl(a, src, LSM_WAVE), rb_ = __shfl(b, src, LSM_WAVE);
+                        fs[3] += 1;
+                        fs[4] += rb_ - ra_;
+                        for (uint32_t k = ra_ + lane; k < rb_; k += LSM_WAVE)
                             top2_add(sqd(lsm_ld(G.xyz, k), qx, qy, qz), int(k), t2);
                     }
-                    wave_top2(t2);
                 }
-                // every unscanned point lies outside the block cube [qb - r, qb + r]
+                wave_top2(t2);
+                // every unscanned point lies outside the block cube [qb - rb, qb + rb]
+                const int r = rb;
                 float bound = INFINITY;
                 if (qbx - r > 0) bound = fminf(bound, qx - (G.ox + (qbx - r) * B));
                 if (qbx + r + 1 < G.nbx) bound = fminf(bound, G.ox + (qbx + r + 1) * B - qx);
@@ -731,19 +754,25 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
                 if (qbz - r > 0) bound = fminf(bound, qz - (G.oz + (qbz - r) * B));
                 if (qbz + r + 1 < G.nbz) bound = fminf(bound, G.oz + (qbz + r + 1) * B - qz);
                 if (bound == INFINITY || t2.bd2 <= bound * bound * 0.99999f ||
-                    bound >= prm.maxc) {
+                    bound >= prm.maxc || rb >= 4095) {
                     fbound = bound;
                     break;
                 }
+                ra = rb + 1;
+                rb = ra;
             }
         }
         if (lane == 0) {
             const int64_t g = P.src_off + q.i;
             const bool hit = t2.bidx >= 0 && t2.bd2 < prm.maxc2;
+            fs[5] += hit ? 1 : 0;
             corr[g] = hit ? t2.bidx : -1;
             rho[g] = hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound);
         }
     }
+    if (fstats && lane == 0)
+        for (int c = 0; c < 7; ++c)
+            if (fs[c]) atomicAdd(fstats + c, (unsigned long long)fs[c]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1195,9 +1224,9 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     static const bool nn_stats = getenv("LSM_NN_STATS") != nullptr;
     unsigned long long *d_nst = nullptr;
     if (nn_stats) {
-        d_nst = (unsigned long long *)ctx->buf("i_nnstats", size_t(ncnt) * NN_NSTAT * 8);
+        d_nst = (unsigned long long *)ctx->buf("i_nnstats", size_t(ncnt) * (NN_NSTAT + 8) * 8);
         if (!d_nst) return LSM_ENOMEM;
-        LSM_HIP_TRY(ctx, hipMemsetAsync(d_nst, 0, size_t(ncnt) * NN_NSTAT * 8, st));
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_nst, 0, size_t(ncnt) * (NN_NSTAT + 8) * 8, st));
     }
     plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
     const TaskPlan tp{d_plan, d_pref, int(npairs)};
@@ -1237,8 +1266,9 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                                                          d_qn + pass, qcap, d_sqn + pass);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
-        nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass, qcap, d_corr,
-                                                  d_rho);
+        nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(
+            d_ps, d_cd, prm, d_q, d_qn + pass, qcap, d_corr, d_rho,
+            d_nst ? d_nst + size_t(ncnt) * NN_NSTAT + size_t(pass) * 8 : nullptr);
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);
         if (p.method == LSM_P2PLANE)
@@ -1265,7 +1295,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
     for (int k = 0; k < passes; ++k) ctx->event_pool.push_back(pass_ev[size_t(k)]);
     if (d_nst) {   // per pass: searched, rows, runs, bsearch steps, points, K, cold, pending
-        std::vector<unsigned long long> h(size_t(passes) * NN_NSTAT);
+        std::vector<unsigned long long> h(size_t(ncnt) * (NN_NSTAT + 8));
         LSM_HIP_TRY(ctx, hipMemcpy(h.data(), d_nst, h.size() * 8, hipMemcpyDeviceToHost));
         for (int k = 0; k < passes; ++k) {
             const unsigned long long *v = h.data() + size_t(k) * NN_NSTAT;
@@ -1274,6 +1304,12 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                     "nnstat pass %2d: searched %9llu rows %.2f runs %.2f bsearch %.2f points %.2f "
                     "K %.2f cold %.3f pending %.4f\n",
                     k, v[0], v[1] / q, v[2] / q, v[3] / q, v[4] / q, v[5] / q, v[6] / q, v[7] / q);
+            const unsigned long long *f = h.data() + size_t(ncnt) * NN_NSTAT + size_t(k) * 8;
+            const double fq = double(std::max(f[0], 1ull));
+            fprintf(stderr,
+                    "fbstat pass %2d: queries %8llu rings %.2f chunks %.2f blocks %.2f points "
+                    "%.1f hits %.3f outside %.3f\n",
+                    k, f[0], f[1] / fq, f[2] / fq, f[3] / fq, f[4] / fq, f[5] / fq, f[6] / fq);
         }
     }
     double nn_bytes = 0.0;
