@@ -50,7 +50,8 @@ def parse():
                     help="hdl64_seq: independent contexts (HIP streams) per GPU, each registering a "
                          "contiguous run of the pairs from its own host thread, so one run's "
                          "latency-bound ICP passes overlap another's normal estimation")
-    ap.add_argument("--cpu-sample-pairs", type=int, default=2)
+    ap.add_argument("--cpu-sample-pairs", type=int, default=6,
+                    help="bounded CPU-oracle sample (~10 s on 16 cores for hdl64_seq)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
