@@ -297,6 +297,31 @@ def test_certified_passes_bit_identical(dev, method, max_corr, monkeypatch):
         _release(dev, ids)
 
 
+def test_certified_split_searches_bit_identical_on_bench_sequence(dev, monkeypatch):
+    """The bench's own data (seed-3 HDL-64 sequence), 24 pairs: enough pairs that the later
+    passes leave workgroups with few uncertified queries, whose box searches are split over
+    2-8 lanes (nn_kernel, group_top2), and enough non-converging pairs to run the 30-update
+    tail. Every result and the final correspondences must equal LSM_NN_NOCERT=1 (one lane per
+    query, every query searched every pass) bit for bit."""
+    seq = synthetic.make_sequence(25, seed=3, model=synthetic.HDL64)
+    ids = _prep(dev, seq.scans, want_normals=True)
+    try:
+        prm = _lib.icp_params(method="p2plane")
+        cert = dev.icp_batch(ids[1:], ids[:-1], seq.priors, prm)
+        c_cert = dev.last_correspondences()
+        monkeypatch.setenv("LSM_NN_NOCERT", "1")
+        full = dev.icp_batch(ids[1:], ids[:-1], seq.priors, prm)
+        c_full = dev.last_correspondences()
+        monkeypatch.delenv("LSM_NN_NOCERT")
+        for a, b in zip(cert, full):
+            assert np.array_equal(a["transformation"], b["transformation"])
+            assert a["fitness"] == b["fitness"] and a["inlier_rmse"] == b["inlier_rmse"]
+            assert a["iterations"] == b["iterations"]
+        assert np.array_equal(c_cert, c_full)
+    finally:
+        _release(dev, ids)
+
+
 # ------------------------------------------------------------------ multi-scale chain (C5)
 @pytest.mark.parametrize("method", ["p2plane", "p2p"])
 def test_multiscale_ouster_pair(dev, method):
