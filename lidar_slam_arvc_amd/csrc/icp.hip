@@ -241,7 +241,8 @@ constexpr int PLAN_THREADS = 1024;
 
 __global__ void __launch_bounds__(PLAN_THREADS)
 plan_kernel(const PairState *__restrict__ st, int npairs, int32_t *__restrict__ pref,
-            int32_t *__restrict__ plan) {
+            int32_t *__restrict__ plan, const uint32_t *__restrict__ active = nullptr,
+            int32_t *poll = nullptr) {
     __shared__ int32_t wsum[PLAN_THREADS / LSM_WAVE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int32_t carry = 0;
@@ -269,6 +270,11 @@ plan_kernel(const PairState *__restrict__ st, int npairs, int32_t *__restrict__ 
         pref[0] = 0;
         plan[0] = carry;
         plan[1] = (carry + NXCD - 1) / NXCD;
+        if (poll) {   // host-mapped pinned words the host polls (no copy dispatches per pass)
+            __hip_atomic_store(poll, int32_t(*active), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(poll + 1, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+        }
     }
 }
 
@@ -1209,6 +1215,14 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int grid = int(std::max<int64_t>(per0 * NXCD, NXCD));
     int32_t *h_poll = (int32_t *)ctx->host_pinned(size_t(ncnt) * 3 * 4);
     if (!h_poll) return LSM_ENOMEM;
+    // LSM_POLL_COPY=1: read the poll words back with two copies per pass (the old path) instead
+    // of plan_kernel storing them into the mapped pinned buffer
+    static const bool poll_copy = getenv("LSM_POLL_COPY") && atoi(getenv("LSM_POLL_COPY")) != 0;
+    int32_t *d_poll = nullptr;
+    if (!poll_copy) {
+        std::memset(h_poll, 0xff, size_t(ncnt) * 3 * 4);
+        LSM_HIP_TRY(ctx, hipHostGetDevicePointer((void **)&d_poll, h_poll, 0));
+    }
     std::vector<hipEvent_t> pass_ev(size_t(ncnt), nullptr);
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
     static const int PASS_LAG = [] {   // passes queued ahead of the last one read back
@@ -1283,11 +1297,16 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                                                        d_active + pass, d_bytes + pass,
                                                        d_srcn + pass, d_flags);
         ctx->toc("solve", ev);
-        plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass, d_active + pass, 4,
-                                        hipMemcpyDeviceToHost, st));
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass + 1, d_plan, 4, hipMemcpyDeviceToHost,
-                                        st));
+        if (d_poll) {
+            plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan,
+                                                    d_active + pass, d_poll + 3 * pass);
+        } else {
+            plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass, d_active + pass, 4,
+                                            hipMemcpyDeviceToHost, st));
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass + 1, d_plan, 4,
+                                            hipMemcpyDeviceToHost, st));
+        }
         pass_ev[size_t(pass)] = ctx->get_event();
         LSM_HIP_TRY(ctx, hipEventRecord(pass_ev[size_t(pass)], st));
         ++passes;
