@@ -34,6 +34,8 @@ extern "C" {
 #define LSM_ESTATE (-4)   /* object in the wrong state (e.g. P2Plane target without normals) */
 #define LSM_ENODEV (-5)   /* no usable gfx950 device */
 
+#define LSM_MAX_ITERATION (1 << 20) /* bound on lsm_icp_params.max_iteration (LSM_EINVAL above) */
+
 #define LSM_P2P 0     /* TransformationEstimationPointToPoint  (keyframe.py:246-248) */
 #define LSM_P2PLANE 1 /* TransformationEstimationPointToPlane  (keyframe.py:249-252) */
 
@@ -153,6 +155,10 @@ int lsm_split_plane(lsm_ctx *ctx, lsm_cloud cloud, const double plane[4], double
  * them, n x 33 f64 in reference order. */
 int lsm_fpfh(lsm_ctx *ctx, lsm_cloud cloud, double radius, int32_t max_nn, double *features,
              int64_t cap);
+/* Feature.data of the features lsm_fpfh computed last (o3d.pipelines.registration.Feature, read
+ * by keyframe.py:318-321 through registration_ransac_based_on_feature_matching): a download only,
+ * n x 33 f64 in reference order; never recomputes. LSM_ESTATE when the cloud has none. */
+int lsm_fpfh_download(lsm_ctx *ctx, lsm_cloud cloud, double *features, int64_t cap);
 /* The feature matches of registration_ransac_based_on_feature_matching (keyframe.py:318-327):
  * every source feature's exact nearest target feature; with `mutual`, only the mutual pairs
  * unless fewer than 3 * ransac_n remain. corres: (source, target) index pairs (reference order),

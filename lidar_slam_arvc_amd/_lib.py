@@ -26,7 +26,7 @@ EXPORTED = [
     "lsm_cloud_voxel_keys", "lsm_icp", "lsm_icp_batch", "lsm_icp_last_correspondences",
     "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
     "lsm_reset_stats", "lsm_ground_plane", "lsm_plane_samples_get", "lsm_split_plane",
-    "lsm_fpfh", "lsm_feature_correspondences", "lsm_ransac_feature",
+    "lsm_fpfh", "lsm_fpfh_download", "lsm_feature_correspondences", "lsm_ransac_feature",
 ]
 
 
@@ -94,6 +94,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "lsm_plane_samples_get": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, _i32p]),
         "lsm_split_plane": (C.c_int, [_P, C.c_int64, _f64p, C.c_double, _i64p, _i64p]),
         "lsm_fpfh": (C.c_int, [_P, C.c_int64, C.c_double, C.c_int32, _f64p, C.c_int64]),
+        "lsm_fpfh_download": (C.c_int, [_P, C.c_int64, _f64p, C.c_int64]),
         "lsm_feature_correspondences": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int32, C.c_int32,
                                                   _i32p, C.c_int64, _i64p]),
         "lsm_ransac_feature": (C.c_int, [_P, C.c_int64, C.c_int64, _i32p, C.c_int64, C.c_double,
@@ -213,6 +214,14 @@ class Device:
         self.check(self.lib.lsm_fpfh(self.handle, int(cloud), float(radius), int(max_nn),
                                      _ptr(out, C.c_double) if download else None, n),
                    "compute_fpfh_feature")
+        return out
+
+    def fpfh_download(self, cloud: int):
+        """The features the last fpfh() call computed (n x 33, reference order); no recompute."""
+        n = self.info(cloud)[1]
+        out = np.zeros((n, 33))
+        self.check(self.lib.lsm_fpfh_download(self.handle, int(cloud), _ptr(out, C.c_double), n),
+                   "lsm_fpfh_download")
         return out
 
     def feature_correspondences(self, src: int, tgt: int, mutual=True, ransac_n=3):

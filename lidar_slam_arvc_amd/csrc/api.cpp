@@ -191,20 +191,30 @@ static int upload_common(lsm_ctx *ctx, const void *xyz, int64_t n, bool f64, lsm
         ctx->set_error("hipMalloc failed for raw cloud");
         return LSM_ENOMEM;
     }
+    // every early return below frees the cloud (no leak of the handle-less allocation)
+    auto fail = [&](hipError_t e, const char *what) {
+        ctx->set_error(std::string(what) + ": " + hipGetErrorString(e));
+        free_cloud(c);
+        return LSM_EHIP;
+    };
+    hipError_t e = hipSuccess;
     if (n > 0) {
         if (!f64) {
-            LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_raw, xyz, size_t(n) * 12, hipMemcpyHostToDevice,
-                                            ctx->stream));
+            e = hipMemcpyAsync(c->d_raw, xyz, size_t(n) * 12, hipMemcpyHostToDevice, ctx->stream);
+            if (e != hipSuccess) return fail(e, "hipMemcpyAsync (upload)");
         } else {
             std::vector<float> tmp(size_t(n) * 3);
             const double *d = static_cast<const double *>(xyz);
             for (size_t i = 0; i < tmp.size(); ++i) tmp[i] = float(d[i]);
-            LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_raw, tmp.data(), tmp.size() * 4,
-                                            hipMemcpyHostToDevice, ctx->stream));
-            LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            e = hipMemcpyAsync(c->d_raw, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice,
+                               ctx->stream);
+            if (e != hipSuccess) return fail(e, "hipMemcpyAsync (upload)");
+            e = hipStreamSynchronize(ctx->stream);
+            if (e != hipSuccess) return fail(e, "hipStreamSynchronize (upload)");
         }
     }
-    LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return fail(e, "hipStreamSynchronize (upload)");
     int64_t id = ctx->next_id++;
     ctx->clouds[id] = c;
     *out = id;
@@ -235,10 +245,16 @@ int lsm_cloud_clone(lsm_ctx *ctx, lsm_cloud src, lsm_cloud *out) {
         ctx->set_error("hipMalloc failed for raw cloud");
         return LSM_ENOMEM;
     }
+    hipError_t e = hipSuccess;
     if (s->n_raw > 0)
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_raw, s->d_raw, size_t(s->n_raw) * 12,
-                                        hipMemcpyDeviceToDevice, ctx->stream));
-    LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        e = hipMemcpyAsync(c->d_raw, s->d_raw, size_t(s->n_raw) * 12, hipMemcpyDeviceToDevice,
+                           ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        ctx->set_error(std::string("lsm_cloud_clone: ") + hipGetErrorString(e));
+        free_cloud(c);
+        return LSM_EHIP;
+    }
     const int64_t id = ctx->next_id++;
     ctx->clouds[id] = c;
     *out = id;
@@ -328,6 +344,27 @@ int lsm_fpfh(lsm_ctx *ctx, lsm_cloud cloud, double radius, int32_t max_nn, doubl
         LSM_HIP_TRY(ctx, hipMemcpy(features, c->d_fpfh, size_t(std::min<int64_t>(cap, c->n)) * 33 * 8,
                                    hipMemcpyDeviceToHost));
     }
+    return LSM_OK;
+}
+
+int lsm_fpfh_download(lsm_ctx *ctx, lsm_cloud cloud, double *features, int64_t cap) {
+    if (!ctx || (cap > 0 && !features) || cap < 0) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!c->d_fpfh || c->fpfh_n != c->n) {
+        ctx->set_error("the cloud has no FPFH features (lsm_fpfh first)");
+        return LSM_ESTATE;
+    }
+    if (cap < c->n) {
+        ctx->set_error("output capacity smaller than the feature count");
+        return LSM_EINVAL;
+    }
+    (void)hipSetDevice(ctx->device);
+    if (c->n > 0)
+        LSM_HIP_TRY(ctx, hipMemcpy(features, c->d_fpfh, size_t(c->n) * 33 * 8, hipMemcpyDeviceToHost));
     return LSM_OK;
 }
 
@@ -503,8 +540,8 @@ static int check_icp(lsm_ctx *ctx, const lsm_icp_params *p) {
         ctx->set_error("unknown transformation estimation method");
         return LSM_EINVAL;
     }
-    if (p->max_iteration < 0) {
-        ctx->set_error("max_iteration must be >= 0");
+    if (p->max_iteration < 0 || p->max_iteration > LSM_MAX_ITERATION) {
+        ctx->set_error("max_iteration must be in [0, 2^20]");
         return LSM_EINVAL;
     }
     return LSM_OK;

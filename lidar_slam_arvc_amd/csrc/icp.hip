@@ -235,6 +235,7 @@ struct TaskPlan {
     const int32_t *plan;   // [0] active blocks, [1] per-lane blocks
     const int32_t *pref;   // [npairs + 1] prefix of the active pairs' block counts
     int npairs;
+    int32_t *err;          // set by a one-task-per-workgroup kernel launched on too small a grid
 };
 
 constexpr int PLAN_THREADS = 1024;
@@ -529,6 +530,10 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
     // one task per workgroup: the host sizes the grid from an earlier pass's plan, which only
     // shrinks, so waves may retire early (no barrier follows the compaction)
     BlockTask task;
+    // the host sizes the grid from a plan it polled; a grid smaller than the current plan would
+    // skip correspondence tasks silently, so it is flagged (the host then fails the batch)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && int64_t(gridDim.x) < int64_t(tp.plan[1]) * NXCD)
+        atomicOr(tp.err, 1);
     if (plan_task(tp, st, blockIdx.x, task) <= 0) return;
     const PairState &P = st[task.pair];
     if (!P.active) return;
@@ -1165,8 +1170,9 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int32_t *d_pref = (int32_t *)ctx->buf("i_pref", size_t(npairs + 1) * 4);
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
+    int32_t *d_err = (int32_t *)ctx->buf("i_err", 4);
     if (!d_corr || !d_rho || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
-        !d_plan || !d_flags) {
+        !d_plan || !d_flags || !d_err) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
     }
@@ -1174,6 +1180,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     uint32_t *d_active = d_counters + ncnt; // [ncnt] active pairs after each pass
     uint32_t *d_sqn = d_counters + 2 * ncnt; // [ncnt] uncertified queries per pass
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_counters, 0, size_t(ncnt) * 3 * 4, st));
+    LSM_HIP_TRY(ctx, hipMemsetAsync(d_err, 0, 4, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_bytes, 0, size_t(ncnt) * 8, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_srcn, 0, size_t(ncnt) * 8, st));
     if (src_off > 0) LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
@@ -1224,6 +1231,16 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         LSM_HIP_TRY(ctx, hipHostGetDevicePointer((void **)&d_poll, h_poll, 0));
     }
     std::vector<hipEvent_t> pass_ev(size_t(ncnt), nullptr);
+    int passes = 0, polled = 0;
+    // the recorded pass events go back to the context's pool on every return, early ones included
+    struct EventReturn {
+        lsm_ctx *ctx;
+        std::vector<hipEvent_t> &ev;
+        const int &n;
+        ~EventReturn() {
+            for (int k = 0; k < n; ++k) ctx->event_pool.push_back(ev[size_t(k)]);
+        }
+    } ev_return{ctx, pass_ev, passes};
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
     static const int PASS_LAG = [] {   // passes queued ahead of the last one read back
         const char *e = getenv("LSM_PASS_LAG");
@@ -1243,8 +1260,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         LSM_HIP_TRY(ctx, hipMemsetAsync(d_nst, 0, size_t(ncnt) * (NN_NSTAT + 8) * 8, st));
     }
     plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
-    const TaskPlan tp{d_plan, d_pref, int(npairs)};
-    int passes = 0, polled = 0;
+    const TaskPlan tp{d_plan, d_pref, int(npairs), d_err};
     int64_t queries = 0, queries0 = 0;   // source points searched (timing mode only)
     for (int pass = 0; pass <= max_iter; ++pass) {
         // newest active-pair counts that have landed; waits only to keep at most PASS_LAG
@@ -1258,7 +1274,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             }
             const int32_t blocks_left = h_poll[3 * polled + 1];
             if (h_poll[3 * polled] == 0) done = true;
-            grid = int(std::max<int64_t>(((int64_t(blocks_left) + NXCD - 1) / NXCD) * NXCD, NXCD));
+            // the plan only shrinks; a word that has not landed (-1 sentinel) keeps the grid
+            if (blocks_left >= 0)
+                grid = int(std::max<int64_t>(((int64_t(blocks_left) + NXCD - 1) / NXCD) * NXCD,
+                                             NXCD));
             ++polled;
         }
         if (done) break;
@@ -1312,7 +1331,14 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         ++passes;
     }
     LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-    for (int k = 0; k < passes; ++k) ctx->event_pool.push_back(pass_ev[size_t(k)]);
+    {
+        int32_t herr = 0;
+        LSM_HIP_TRY(ctx, hipMemcpy(&herr, d_err, 4, hipMemcpyDeviceToHost));
+        if (herr) {
+            ctx->set_error("internal: correspondence pass launched on a grid smaller than its plan");
+            return LSM_EHIP;
+        }
+    }
     if (d_nst) {   // per pass: searched, rows, runs, bsearch steps, points, K, cold, pending
         std::vector<unsigned long long> h(size_t(ncnt) * (NN_NSTAT + 8));
         LSM_HIP_TRY(ctx, hipMemcpy(h.data(), d_nst, h.size() * 8, hipMemcpyDeviceToHost));

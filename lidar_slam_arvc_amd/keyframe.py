@@ -64,17 +64,22 @@ class HostPointCloud:
 
 
 class FeatureHandle:
-    """The FPFH features of a device cloud (o3d Feature: ``.data`` 33 x N), fetched lazily."""
+    """The FPFH features of a device cloud (o3d Feature: ``.data`` 33 x N), fetched lazily.
 
-    def __init__(self, dev, handle):
+    ``radius`` / ``max_nn`` record the KDTreeSearchParamHybrid the features were computed with;
+    reading ``.data`` only downloads them (lsm_fpfh_download) and never recomputes."""
+
+    def __init__(self, dev, handle, radius, max_nn):
         self._dev = dev
         self._handle = handle
+        self.radius = radius
+        self.max_nn = max_nn
         self._data = None
 
     @property
     def data(self):
         if self._data is None:
-            self._data = self._dev.fpfh(self._handle, 0.3, 100).T
+            self._data = self._dev.fpfh_download(self._handle).T
         return self._data
 
 
@@ -210,11 +215,17 @@ class KeyFrame:
                                 normal_radius=self.voxel_size_normals,
                                 max_nn=ICP_PARAMETERS.max_nn, want_normals=normals)
 
+    def _key(self, radii, heights, voxel, normals):
+        """Cache key of a processed cloud: every parameter the device pass depends on."""
+        r = radii if radii is not None else (self.min_radius, self.max_radius)
+        h = heights if heights is not None else (self.min_height, self.max_height)
+        nk = (self.voxel_size_normals, ICP_PARAMETERS.max_nn) if normals else None
+        return (tuple(r), tuple(h), voxel, normals, nk)
+
     def _run(self, radii, heights, voxel, normals):
         if self._handle is None:
             raise RuntimeError("KeyFrame has no point cloud loaded (call load_pointcloud)")
-        key = (tuple(radii) if radii is not None else None,
-               tuple(heights) if heights is not None else None, voxel, normals)
+        key = self._key(radii, heights, voxel, normals)
         if key != self._prep_key:
             self._dev.preprocess([self._handle], self._params(radii, heights, voxel, normals))
             self._prep_key = key
@@ -256,7 +267,8 @@ class KeyFrame:
                                       "keyframe.py:193-203) is not on the MI355X path")
         self.preprocess_icp2planes()        # filter, normals, plane, split, part normals
         self._dev.fpfh(self._planes[1], self.voxel_size_normals, 100, download=False)
-        self.pointcloud_fpfh = FeatureHandle(self._dev, self._planes[1])
+        self.pointcloud_fpfh = FeatureHandle(self._dev, self._planes[1], self.voxel_size_normals,
+                                             100)
 
     def global_registration(self, other):
         """RANSAC on the non-ground parts' FPFH matches, then P2Plane ICP of the filtered clouds

@@ -63,15 +63,24 @@ class KeyFrameManager:
             for kf in kfs:
                 kf.pre_process(method=self.method)
             return
+        from .keyframe import DevicePointCloud
         normals = self.method == "icppointplane"
-        todo = [kf for kf in kfs if kf._prep_key != (None, None, kf.voxel_size, normals)]
-        if todo:
-            prm = todo[0]._params(None, None, self.voxel_size, normals)
-            self._dev.preprocess([kf._handle for kf in todo], prm)
+        # one device pass per distinct parameter set (each keyframe keeps its own voxel size,
+        # normal radius and filter bounds, exactly as KeyFrame.pre_process would use them)
+        groups = {}
         for kf in kfs:
-            kf._prep_key = (None, None, kf.voxel_size, normals)
+            if kf._handle is None:
+                raise RuntimeError("KeyFrame has no point cloud loaded (call load_pointcloud)")
+            key = kf._key(None, None, kf.voxel_size, normals)
+            if kf._prep_key != key:
+                groups.setdefault(key, []).append(kf)
+        for key, group in groups.items():
+            prm = group[0]._params(None, None, group[0].voxel_size, normals)
+            self._dev.preprocess([kf._handle for kf in group], prm)
+            for kf in group:
+                kf._prep_key = key
+        for kf in kfs:
             kf._filter = (None, None)
-            from .keyframe import DevicePointCloud
             kf.pointcloud_filtered = DevicePointCloud(self._dev, kf._handle, normals)
 
     # ------------------------------------------------------------------ registration

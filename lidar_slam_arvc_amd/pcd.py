@@ -3,8 +3,11 @@
 Reads x, y, z of PCD v0.7 files in DATA ascii / binary / binary_compressed (LZF), the three
 encodings Open3D's reader accepts. As Open3D does by default (remove_nan_points=False), NaN/inf
 points are kept; they are dropped by filter_radius_height because every comparison with NaN is
-false (keyframe.py:92). Returns float32 N x 3 (the on-disk precision; Open3D widens to float64
-exactly). A ``write_pcd`` helper produces test fixtures and synthetic datasets.
+false (keyframe.py:92). Returns float32 N x 3. For SIZE 4 binary fields this is the on-disk
+precision (Open3D widens it to float64 exactly). SIZE 8 fields and ascii values are ROUNDED to
+float32 here, while Open3D keeps them in float64: the device path stores f32 coordinates, so for
+such files parity with the reference is unpinned beyond that rounding.
+A ``write_pcd`` helper produces test fixtures and synthetic datasets.
 """
 from __future__ import annotations
 
