@@ -5,6 +5,7 @@ synthetic input already resident in HBM: pre-process P+1 keyframes (filter_radiu
 estimate_normals, keyframe.py:156-162), register the P consecutive pairs with point-to-plane ICP
 (keyframe.py:249-252, Open3D criteria), fetch the P relative transforms to the host and compose
 the global poses (homogeneousmatrix.py:184-205; RCCL all-gather of chunk totals when N > 1).
+The default P = 1999 is BASELINE.json's C3 workload, a 2000-keyframe sequence on one GPU.
 Weak scaling: every GPU owns P pairs of one long sequence (distributed.py).
 
     python bench.py [--gpus N --steps K --warmup W --pairs-per-gpu P]
@@ -43,7 +44,8 @@ def parse():
                          "ouster_multiscale: C5 256k Ouster-128, voxel 0.4/0.2/0.1 m chain; "
                          "loop_closure: C4 independent 64k revisit pairs (sharded, no halo)")
     ap.add_argument("--pairs-per-gpu", type=int, default=0,
-                    help="0: 256 (hdl64), 32 (ouster), 512 (loop_closure)")
+                    help="0: 1999 (hdl64: the C3 2000-keyframe sequence), 32 (ouster), "
+                         "512 (loop_closure: C4's 4096 pairs over 8 GPUs)")
     ap.add_argument("--seed", type=int, default=-1, help="-1: 3 (hdl64), 5 (ouster)")
     ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
     ap.add_argument("--streams", type=int, default=1,
@@ -55,7 +57,25 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
+    ap.add_argument("--seq-cache", default="",
+                    help="A/B runs (hdl64_seq): load the synthetic sequence from this .npz if it "
+                         "exists, else generate it and save it there")
     return ap.parse_args()
+
+
+def load_or_make_sequence(path, P, seed, model, first, procs):
+    from lidar_slam_arvc_amd import synthetic
+    tag = f"{P}_{seed}_{model.rings}x{model.azimuths}_{first}"
+    if path and os.path.exists(path):
+        z = np.load(path)
+        if str(z["tag"]) == tag:
+            return synthetic.Sequence([z[f"s{k}"] for k in range(P + 1)], z["poses"], z["priors"])
+    seq = synthetic.make_sequence(P + 1, seed=seed, model=model, first_index=first,
+                                  processes=procs)
+    if path:
+        np.savez(path, tag=tag, poses=seq.poses, priors=seq.priors,
+                 **{f"s{k}": s for k, s in enumerate(seq.scans)})
+    return seq
 
 
 def cpu_baseline(seq, n_pairs: int, method: str, threads: int):
@@ -118,6 +138,26 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    from lidar_slam_arvc_amd import synthetic
+
+    ouster = args.workload == "ouster_multiscale"
+    loop = args.workload == "loop_closure"
+    P = args.pairs_per_gpu or (32 if ouster else (512 if loop else 1999))
+    first = rank * P
+    model = synthetic.OUSTER128 if ouster else synthetic.HDL64
+    seed = args.seed if args.seed >= 0 else (5 if ouster else (4 if loop else 3))
+    # synthetic scans first, in forked worker processes: nothing in this process has touched the
+    # GPU yet (a fork after HIP initialisation is not safe)
+    procs = max(1, min(8, os.cpu_count() or 1))
+    if loop:
+        # C4: every rank owns P independent revisit pairs (its own targets and sources)
+        ps = synthetic.make_revisit_pairs(P, seed=seed, model=model, first_index=first,
+                                          processes=procs)
+        seq = synthetic.Sequence(ps.targets + ps.sources, np.zeros((0, 4, 4)), ps.init)
+        del ps
+    else:
+        seq = load_or_make_sequence(args.seq_cache, P, seed, model, first, procs)
+
     import torch
     import torch.distributed as dist
 
@@ -127,25 +167,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         group = dist.group.WORLD
 
-    from lidar_slam_arvc_amd import _lib, synthetic
+    from lidar_slam_arvc_amd import _lib
     from lidar_slam_arvc_amd.distributed import compose_global_sharded
 
     extra_ids = []                                   # (context, handle) of extra runs
     devs = [None]
-    ouster = args.workload == "ouster_multiscale"
-    loop = args.workload == "loop_closure"
-    P = args.pairs_per_gpu or (32 if ouster else (512 if loop else 256))
-    first = rank * P
-    model = synthetic.OUSTER128 if ouster else synthetic.HDL64
-    seed = args.seed if args.seed >= 0 else (5 if ouster else (4 if loop else 3))
     dev = _lib.device(local)
-    if loop:
-        # C4: every rank owns P independent revisit pairs (its own targets and sources)
-        ps = synthetic.make_revisit_pairs(P, seed=seed, model=model, first_index=first)
-        seq = synthetic.Sequence(ps.targets + ps.sources, np.zeros((0, 4, 4)), ps.init)
-        del ps
-    else:
-        seq = synthetic.make_sequence(P + 1, seed=seed, model=model, first_index=first)
     ids = [dev.upload(s) for s in seq.scans]        # raw scans resident in HBM
     want_normals = args.method == "p2plane"
     cuda = torch.device("cuda", local)

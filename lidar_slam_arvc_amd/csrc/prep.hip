@@ -574,6 +574,37 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
     }
 }
 
+// scan_run with the window test folded into a predicate: body(p, k, in) is called for every
+// loaded point until the walk passes xh, `in` telling whether it lies in the window (fewer
+// divergent branches per point than nested ifs).
+template <int G, typename Body>
+__device__ __forceinline__ void scan_run_pred(const float4 *xyz, uint32_t a, uint32_t b, float xl,
+                                              float xh, Body &&body) {
+    if (b - a > SCAN_BSEARCH) {
+        uint32_t lo = a, hi = b;
+        const float *xs = reinterpret_cast<const float *>(xyz);
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (lsm_ld(xs, size_t(mid) * 4) < xl) lo = mid + 1;
+            else hi = mid;
+        }
+        a = lo;
+    }
+    static_assert(G <= LSM_XYZ_PAD, "group loads may run LSM_XYZ_PAD points past a run");
+    for (uint32_t k = a; k < b; k += G) {
+        float4 p[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) p[g] = lsm_ld(xyz, k + uint32_t(g));
+        bool live = true;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            live = live && (k + uint32_t(g) < b) && !(p[g].x > xh);
+            body(p[g], k + uint32_t(g), live && p[g].x >= xl);
+        }
+        if (!live) break;
+    }
+}
+
 // Exact kNN truncation (Open3D SearchHybrid keeps the max_nn nearest of the ball, ordered by
 // (d2, traversal); here by (d2, sorted index)), one lane per point, no cross-lane traffic.
 //
@@ -701,15 +732,14 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // rounding band, bin edges) take the exact f64 distance, so the histogram is the one the
     // f64 binning of the later scans implies.
     ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+        scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
             const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
             const float f = dx * dx + dy * dy + dz * dz;
             const float t = f * np.hscale;
             const float fr = t - floorf(t);
-            int bb = -1;
-            if (f < np.r2_lo && fr > 2e-4f && fr < 1.f - 2e-4f) {
-                bb = int(t);
-            } else if (f <= np.r2_hi) {
+            const bool fast = in && f < np.r2_lo && fr > 2e-4f && fr < 1.f - 2e-4f;
+            int bb = fast ? int(t) : -1;
+            if (in && !fast && f <= np.r2_hi) {   // the sphere's rounding band, bin edges
                 const Off o = make_off(p, qx, qy, qz);
                 if (o.d2 < np.r2) bb = sel_level_bin(S, o.d2, k);
             }
@@ -753,9 +783,9 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         kmin = 0xffffffffu;
         kmax = 0u;
         ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
-            scan_run<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+            scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
                 Off o;
-                if (in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
+                if (in && in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
                     lds_add(H + sel_level_bin(next, o.d2, k), 1u);
                     dmin = fmin(dmin, o.d2);
                     dmax = fmax(dmax, o.d2);
@@ -829,9 +859,9 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // final pass: everything below, plus the `need` smallest members
     uint32_t m = 0;
     ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k) {
+        scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
             const float fd = f32_d2(qf, p);
-            if (fd > np.r2_hi) return;
+            if (!in || fd > np.r2_hi) return;
             const Off o = make_off(p, qx, qy, qz);
             if (fd >= np.r2_lo && !(o.d2 < np.r2)) return;
             const int cl = sel_classify(S, o.d2, k);
@@ -955,7 +985,9 @@ int ensure_cloud_buffers(lsm_ctx *ctx, Cloud *c, int64_t n, bool normals) {
         c->d_nrm = nullptr;
         c->d_perm = nullptr;
         int64_t cap = std::max<int64_t>(n, 1);
-        if (hipMalloc(&c->d_xyz, cap * sizeof(float4)) != hipSuccess ||
+        // LSM_XYZ_PAD spare points past the end: the normals walks load whole groups without
+        // clamping the index (the spare lanes' values are never used)
+        if (hipMalloc(&c->d_xyz, (cap + LSM_XYZ_PAD) * sizeof(float4)) != hipSuccess ||
             hipMalloc(&c->d_perm, cap * sizeof(uint32_t)) != hipSuccess) {
             ctx->set_error("hipMalloc failed for processed cloud");
             return LSM_ENOMEM;

@@ -155,14 +155,114 @@ def perturb(T: np.ndarray, rng: np.random.Generator, sigma_t: float, sigma_rot_d
     return T @ D
 
 
+def _box_hits(d: np.ndarray, o: np.ndarray, bx: np.ndarray) -> np.ndarray:
+    """Nearest slab-test hit of each ray (rows of d) over the boxes bx (inf: none)."""
+    if not len(bx) or not len(d):
+        return np.full(len(d), np.inf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / d
+        t1 = (bx[None, :, 0:3] - o[None, None, :]) * inv[:, None, :]
+        t2 = (bx[None, :, 3:6] - o[None, None, :]) * inv[:, None, :]
+    tmin = np.nanmax(np.minimum(t1, t2), axis=2)
+    tmax = np.nanmin(np.maximum(t1, t2), axis=2)
+    ok = (tmax >= np.maximum(tmin, 1e-6))
+    tb = np.where(ok, np.where(tmin > 1e-6, tmin, np.inf), np.inf)
+    return tb.min(axis=1)
+
+
+def _pole_hits(d: np.ndarray, o: np.ndarray, pl: np.ndarray) -> np.ndarray:
+    """Nearest hit of each ray on the vertical cylinders pl (inf: none)."""
+    if not len(pl) or not len(d):
+        return np.full(len(d), np.inf)
+    ox = o[0] - pl[None, :, 0]
+    oy = o[1] - pl[None, :, 1]
+    a2 = (d[:, 0:1] ** 2 + d[:, 1:2] ** 2)
+    b2 = 2.0 * (ox * d[:, 0:1] + oy * d[:, 1:2])
+    c2 = ox * ox + oy * oy - pl[None, :, 2] ** 2
+    disc = b2 * b2 - 4.0 * a2 * c2
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tc = (-b2 - np.sqrt(np.maximum(disc, 0.0))) / (2.0 * a2)
+    z = o[2] + tc * d[:, 2:3]
+    okc = (disc > 0) & (tc > 1e-6) & (z >= 0.0) & (z <= pl[None, :, 3])
+    return np.where(okc, tc, np.inf).min(axis=1)
+
+
+N_SECTORS = 64          # azimuth sectors of the culled ray cast
+_ANG_MARGIN = 1e-3      # rad: angular intervals are widened by this much (conservative)
+
+
+def _sector_sets(o: np.ndarray, lo: np.ndarray, hi: np.ndarray, everywhere: np.ndarray) -> list:
+    """Object indices per azimuth sector: object j covers the world azimuths [lo_j, hi_j] (as
+    seen from o, span < pi, possibly wrapping), or every azimuth when everywhere_j."""
+    w = 2.0 * np.pi / N_SECTORS
+    sets = [[] for _ in range(N_SECTORS)]
+    for j in range(len(lo)):
+        if everywhere[j]:
+            for s in range(N_SECTORS):
+                sets[s].append(j)
+            continue
+        s0 = int(math.floor((lo[j] - _ANG_MARGIN + np.pi) / w))
+        s1 = int(math.floor((hi[j] + _ANG_MARGIN + np.pi) / w))
+        for s in range(s0, s1 + 1):
+            sets[s % N_SECTORS].append(j)
+    return [np.asarray(v, dtype=np.int64) for v in sets]
+
+
 def raycast(scene: Scene, pose: np.ndarray, model: LidarModel, rng: np.random.Generator,
             chunk: int = 16384) -> np.ndarray:
-    """Ray-cast one spinning scan; returns float32 M x 3 sensor-frame points (misses removed)."""
+    """Ray-cast one spinning scan; returns float32 M x 3 sensor-frame points (misses removed).
+
+    Rays are grouped by world azimuth sector and tested only against the boxes / poles whose
+    angular extent (seen from the sensor) overlaps the sector. A ray's xy direction must lie
+    inside an object's angular extent to reach its vertical prism, so the culled set always
+    holds the object it hits, and every (ray, object) test is the same arithmetic as the brute
+    force over all objects (``raycast_bruteforce``): the scans are bit-identical to it.
+    """
     d_s = model.directions()
     R, o = pose[:3, :3], pose[:3, 3]
     # d_s R^T without BLAS: this runs in worker threads, and concurrent OpenBLAS calls gave
     # run-to-run different scans on many-core hosts
     d_w = d_s[:, 0:1] * R[:, 0] + d_s[:, 1:2] * R[:, 1] + d_s[:, 2:3] * R[:, 2]
+    bx, pl = _near_objects(scene, o, model)
+    dz = d_w[:, 2]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t_hit = np.where(dz < -1e-9, -o[2] / dz, np.inf)
+    # angular extents of the boxes' xy footprints and of the poles
+    if len(bx):
+        inside = ((o[0] >= bx[:, 0] - 1e-6) & (o[0] <= bx[:, 3] + 1e-6) &
+                  (o[1] >= bx[:, 1] - 1e-6) & (o[1] <= bx[:, 4] + 1e-6))
+        cxs = np.stack([bx[:, 0], bx[:, 3], bx[:, 3], bx[:, 0]], axis=1) - o[0]
+        cys = np.stack([bx[:, 1], bx[:, 1], bx[:, 4], bx[:, 4]], axis=1) - o[1]
+        ref = np.arctan2(cys.mean(axis=1), cxs.mean(axis=1))
+        rel = np.arctan2(cys, cxs) - ref[:, None]
+        rel = (rel + np.pi) % (2.0 * np.pi) - np.pi
+        blo, bhi = ref + rel.min(axis=1), ref + rel.max(axis=1)
+        box_sets = _sector_sets(o, blo, bhi, inside)
+    if len(pl):
+        dist = np.hypot(pl[:, 0] - o[0], pl[:, 1] - o[1])
+        near_pole = dist <= pl[:, 2] * 1.001 + 1e-3
+        half = np.arcsin(np.minimum(1.0, (pl[:, 2] * 1.001 + 1e-3) / np.maximum(dist, 1e-9)))
+        pc = np.arctan2(pl[:, 1] - o[1], pl[:, 0] - o[0])
+        pole_sets = _sector_sets(o, pc - half, pc + half, near_pole)
+    w = 2.0 * np.pi / N_SECTORS
+    sec = np.floor((np.arctan2(d_w[:, 1], d_w[:, 0]) + np.pi) / w).astype(np.int64) % N_SECTORS
+    order = np.argsort(sec, kind="stable")
+    bounds = np.searchsorted(sec[order], np.arange(N_SECTORS + 1))
+    for s in range(N_SECTORS):
+        idx = order[bounds[s]:bounds[s + 1]]
+        if not len(idx):
+            continue
+        d = d_w[idx]
+        best = t_hit[idx]
+        if len(bx):
+            best = np.minimum(best, _box_hits(d, o, bx[box_sets[s]]))
+        if len(pl):
+            best = np.minimum(best, _pole_hits(d, o, pl[pole_sets[s]]))
+        t_hit[idx] = best
+    return _finish_scan(d_s, t_hit, model, rng)
+
+
+def _near_objects(scene: Scene, o: np.ndarray, model: LidarModel):
     near = model.max_range + 3.0
     bx = scene.boxes
     if len(bx):
@@ -172,37 +272,30 @@ def raycast(scene: Scene, pose: np.ndarray, model: LidarModel, rng: np.random.Ge
     pl = scene.poles
     if len(pl):
         pl = pl[(pl[:, 0] - o[0]) ** 2 + (pl[:, 1] - o[1]) ** 2 < near * near]
+    return bx, pl
+
+
+def raycast_bruteforce(scene: Scene, pose: np.ndarray, model: LidarModel,
+                       rng: np.random.Generator, chunk: int = 16384) -> np.ndarray:
+    """``raycast`` without the sector culling (every ray against every near object); kept as
+    the check that the culled ray cast returns the same scans."""
+    d_s = model.directions()
+    R, o = pose[:3, :3], pose[:3, 3]
+    d_w = d_s[:, 0:1] * R[:, 0] + d_s[:, 1:2] * R[:, 1] + d_s[:, 2:3] * R[:, 2]
+    bx, pl = _near_objects(scene, o, model)
     t_hit = np.full(len(d_w), np.inf)
     for a in range(0, len(d_w), chunk):
         d = d_w[a:a + chunk]
-        best = np.full(len(d), np.inf)
         dz = d[:, 2]
         with np.errstate(divide="ignore", invalid="ignore"):
-            tg = np.where(dz < -1e-9, -o[2] / dz, np.inf)
-        best = np.minimum(best, tg)
-        if len(bx):
-            with np.errstate(divide="ignore", invalid="ignore"):
-                inv = 1.0 / d
-                t1 = (bx[None, :, 0:3] - o[None, None, :]) * inv[:, None, :]
-                t2 = (bx[None, :, 3:6] - o[None, None, :]) * inv[:, None, :]
-            tmin = np.nanmax(np.minimum(t1, t2), axis=2)
-            tmax = np.nanmin(np.maximum(t1, t2), axis=2)
-            ok = (tmax >= np.maximum(tmin, 1e-6))
-            tb = np.where(ok, np.where(tmin > 1e-6, tmin, np.inf), np.inf)
-            best = np.minimum(best, tb.min(axis=1))
-        if len(pl):
-            ox = o[0] - pl[None, :, 0]
-            oy = o[1] - pl[None, :, 1]
-            a2 = (d[:, 0:1] ** 2 + d[:, 1:2] ** 2)
-            b2 = 2.0 * (ox * d[:, 0:1] + oy * d[:, 1:2])
-            c2 = ox * ox + oy * oy - pl[None, :, 2] ** 2
-            disc = b2 * b2 - 4.0 * a2 * c2
-            with np.errstate(divide="ignore", invalid="ignore"):
-                tc = (-b2 - np.sqrt(np.maximum(disc, 0.0))) / (2.0 * a2)
-            z = o[2] + tc * d[:, 2:3]
-            okc = (disc > 0) & (tc > 1e-6) & (z >= 0.0) & (z <= pl[None, :, 3])
-            best = np.minimum(best, np.where(okc, tc, np.inf).min(axis=1))
+            best = np.where(dz < -1e-9, -o[2] / dz, np.inf)
+        best = np.minimum(best, _box_hits(d, o, bx))
+        best = np.minimum(best, _pole_hits(d, o, pl))
         t_hit[a:a + chunk] = best
+    return _finish_scan(d_s, t_hit, model, rng)
+
+
+def _finish_scan(d_s, t_hit, model, rng):
     hit = np.isfinite(t_hit) & (t_hit <= model.max_range)
     rng_noise = rng.normal(0.0, model.noise, size=len(d_s))
     t = t_hit + rng_noise
@@ -221,11 +314,13 @@ class Sequence:
 def make_sequence(n_keyframes: int, seed: int = 3, model: LidarModel = HDL64,
                   spacing: float = 0.5, start: float = 0.0, path_length: float = 1000.0,
                   sigma_t: float = 0.05, sigma_rot_deg: float = 1.0,
-                  first_index: int = 0) -> Sequence:
+                  first_index: int = 0, processes: int = 0) -> Sequence:
     """C3-style sequence: keyframes every ``spacing`` metres along a closed loop.
 
     ``first_index`` lets ranks generate disjoint chunks of one global sequence: keyframe ``k``
     always gets the same pose, scan noise and prior no matter which chunk generates it.
+    ``processes`` > 0 ray-casts in that many forked worker processes (only before the GPU is
+    initialised in this process: bench.py); otherwise threads.
     """
     path = loop_path(path_length)
     scene = make_scene(seed, path)
@@ -235,7 +330,7 @@ def make_sequence(n_keyframes: int, seed: int = 3, model: LidarModel = HDL64,
         T = path_pose(path, start + k * spacing, rng)
         return T, raycast(scene, T, model, rng)
 
-    out = _parallel_map(one, range(first_index, first_index + n_keyframes))
+    out = _parallel_map(one, range(first_index, first_index + n_keyframes), processes)
     poses = np.asarray([o[0] for o in out])
     scans = [o[1] for o in out]
     priors = []
@@ -258,7 +353,8 @@ class PairSet:
 
 def make_revisit_pairs(n_pairs: int, seed: int = 4, model: LidarModel = HDL64,
                        path_length: float = 1000.0, sigma_t: float = 0.3,
-                       sigma_yaw_deg: float = 3.0, first_index: int = 0) -> PairSet:
+                       sigma_yaw_deg: float = 3.0, first_index: int = 0,
+                       processes: int = 0) -> PairSet:
     """C4-style pairs: a pose on the loop and a revisit 0.5-2 m / <=10 deg away."""
     path = loop_path(path_length)
     scene = make_scene(seed, path)
@@ -277,17 +373,51 @@ def make_revisit_pairs(n_pairs: int, seed: int = 4, model: LidarModel = HDL64,
         rel = np.linalg.inv(Ti) @ Tj
         return a, b, rel, perturb(rel, rng, sigma_t, sigma_yaw_deg, yaw_only=True)
 
-    out = _parallel_map(one, range(first_index, first_index + n_pairs))
+    out = _parallel_map(one, range(first_index, first_index + n_pairs), processes)
     return PairSet([o[0] for o in out], [o[1] for o in out], np.asarray([o[2] for o in out]),
                    np.asarray([o[3] for o in out]))
 
 
-def _parallel_map(fn, items):
-    """Thread pool map (NumPy releases the GIL in the ray-box kernels); order-preserving."""
+_FORK_FN = None
+
+
+def _fork_call(i):
+    return _FORK_FN(i)
+
+
+def _gpu_initialised() -> bool:
+    """True when this process may already hold a GPU context (so it must not fork): torch or
+    liblidarsm initialised it, or a profiler (rocprofv3 preloads a library that does)."""
+    import os
+    import sys
+    if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(
+            k.startswith("ROCPROF") for k in os.environ):
+        return True
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        return True
+    lib = sys.modules.get("lidar_slam_arvc_amd._lib")
+    return bool(lib is not None and getattr(lib, "_devices", None))
+
+
+def _parallel_map(fn, items, processes: int = 0):
+    """Order-preserving map: forked processes when asked for and safe (no GPU context in this
+    process yet), else a thread pool (the per-sector NumPy calls are small and mostly hold the
+    GIL, so threads gain little)."""
     from concurrent.futures import ThreadPoolExecutor
     import os
     from threadpoolctl import threadpool_limits
     items = list(items)
+    if processes > 1 and len(items) > 1 and not _gpu_initialised():
+        import multiprocessing as mp
+        global _FORK_FN
+        _FORK_FN = fn
+        try:
+            with threadpool_limits(limits=1, user_api="blas"):
+                with mp.get_context("fork").Pool(min(processes, len(items))) as pool:
+                    return pool.map(_fork_call, items, chunksize=4)
+        finally:
+            _FORK_FN = None
     workers = max(1, min(8, os.cpu_count() or 1, len(items)))
     # single-threaded BLAS inside the workers: the small matrix products of the pose math must
     # not race on OpenBLAS's shared buffers (that made scans differ between runs)

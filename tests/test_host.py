@@ -121,6 +121,18 @@ def test_synthetic_determinism_and_chunking():
     assert np.abs(gt[:3, 3] - a.priors[0][:3, 3]).max() < 0.5
 
 
+@pytest.mark.parametrize("model,seed,k", [("VLP16_8K", 21, 0), ("VLP16_8K", 4, 777),
+                                          ("HDL64", 3, 5), ("HDL64", 3, 1999)])
+def test_sector_culled_raycast_is_bit_identical(model, seed, k):
+    m = getattr(synthetic, model)
+    path = synthetic.loop_path(1000.0)
+    scene = synthetic.make_scene(seed, path)
+    T = synthetic.path_pose(path, 0.5 * k, np.random.default_rng([seed, k]))
+    a = synthetic.raycast(scene, T, m, np.random.default_rng([seed, k, 1]))
+    b = synthetic.raycast_bruteforce(scene, T, m, np.random.default_rng([seed, k, 1]))
+    assert a.shape == b.shape and np.array_equal(a, b)
+
+
 # ------------------------------------------------------------------ sharding
 def test_shard_pairs_cover():
     for n in [1, 7, 64, 1999]:
