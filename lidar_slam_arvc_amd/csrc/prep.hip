@@ -385,6 +385,7 @@ struct NormalParams {
     int max_nn;
     float dense_k;    // own cell holds >= dense_k * cell^2 points: predicted > max_nn neighbours
                       // (0: off)
+    int preclass;     // final pass: f32 pre-classification (0: every point takes the f64 test)
 };
 
 // Offsets of a candidate from the query in f64 (exact: both are f32 values) with their squares,
@@ -531,6 +532,7 @@ __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, fl
 // window. Long runs find the window's first point by binary search on x (a run averages ~140
 // points of which ~30 lie left of the window on HDL-64 scans); the walk stops past xh.
 constexpr uint32_t SCAN_BSEARCH = 16;
+constexpr uint32_t SCAN_SLACK = 8;   // scan_run_pred: entry search stops within this many points
 constexpr int NORMALS_G_DEFAULT = 4;
 
 template <int G, typename Body>
@@ -581,12 +583,19 @@ template <int G, typename Body>
 __device__ __forceinline__ void scan_run_pred(const float4 *xyz, uint32_t a, uint32_t b, float xl,
                                               float xh, Body &&body) {
     if (b - a > SCAN_BSEARCH) {
-        uint32_t lo = a, hi = b;
+        // 4-ary search (three probes per round trip) for a start at most SCAN_SLACK points
+        // before the window's first point: the walk skips x < xl anyway
+        uint32_t lo = a, hi = b;   // the first x >= xl lies in [lo, hi]
         const float *xs = reinterpret_cast<const float *>(xyz);
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (lsm_ld(xs, size_t(mid) * 4) < xl) lo = mid + 1;
-            else hi = mid;
+        while (hi - lo > SCAN_SLACK) {
+            const uint32_t q = (hi - lo) >> 2;
+            const uint32_t m1 = lo + q, m2 = lo + 2 * q, m3 = lo + 3 * q;
+            const float x1 = lsm_ld(xs, size_t(m1) * 4), x2 = lsm_ld(xs, size_t(m2) * 4),
+                        x3 = lsm_ld(xs, size_t(m3) * 4);
+            if (x3 < xl) lo = m3 + 1;
+            else if (x2 < xl) { lo = m2 + 1; hi = m3; }
+            else if (x1 < xl) { lo = m1 + 1; hi = m2; }
+            else hi = m1;
         }
         a = lo;
     }
@@ -856,12 +865,29 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         top = fmin(top, dmax);
         S = next;
     }
-    // final pass: everything below, plus the `need` smallest members
+    // final pass: everything below, plus the `need` smallest members. f32 pre-classification:
+    // d2 below min(r2, dlo, the chosen d2 bin's lower edge) is certainly "below", d2 above
+    // max(dhi-side bounds) certainly "above"; only the band between takes the exact f64 test
+    // (the f32 d2 is within 4.2e-7 relative; 2e-6 of margin).
+    // (sel_classify: below iff d2 < dlo or, d2 <= dhi, bin < b; above iff d2 > dhi or, d2 >= dlo,
+    // bin > b -- the bins of d2 levels are monotone in d2 with edges lo + j / scale)
+    double lo_t = S.dlo, hi_t = S.dhi;
+    if (!S.by_idx) {
+        lo_t = fmax(lo_t, fmin(S.dhi, S.lo + double(S.b) / S.scale));
+        if (S.b < S.nb - 1) hi_t = fmin(hi_t, fmax(S.dlo, S.lo + double(S.b + 1) / S.scale));
+    }
+    lo_t = fmin(lo_t, np.r2);   // below also needs d2 < r2
+    const float below32 = np.preclass && lo_t > 0.0 ? float(lo_t * (1.0 - 2e-6)) : -1.f;
+    const float above32 = np.preclass && hi_t < 1e30 ? float(hi_t * (1.0 + 2e-6)) : INFINITY;
     uint32_t m = 0;
     ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
             const float fd = f32_d2(qf, p);
-            if (!in || fd > np.r2_hi) return;
+            if (!in || fd > np.r2_hi || fd > above32) return;
+            if (fd < below32) {
+                acc.add(p, k);
+                return;
+            }
             const Off o = make_off(p, qx, qy, qz);
             if (fd >= np.r2_lo && !(o.d2 < np.r2)) return;
             const int cl = sel_classify(S, o.d2, k);
@@ -905,6 +931,13 @@ float dense_k(int max_nn, double r2) {
     }();
     if (frac <= 0.0 || r2 <= 0.0) return 0.f;
     return float(frac * double(max_nn) / r2);
+}
+
+// LSM_NORMALS_EXACT=1 (read per call): no f32 pre-classification in the final pass -- the tests'
+// proof that it leaves every neighbourhood, and so every normal, bit-identical
+int normals_preclass() {
+    const char *e = getenv("LSM_NORMALS_EXACT");
+    return (e && atoi(e) != 0) ? 0 : 1;
 }
 
 template <int G>
@@ -1398,6 +1431,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         np.hscale = float(double(NB8) / np.r2);
         np.max_nn = p.max_nn;
         np.dense_k = dense_k(p.max_nn, np.r2);
+        np.preclass = normals_preclass();
         ctx->tic("normals", &ev);
         {
             static const bool nstats = getenv("LSM_NORMALS_STATS") != nullptr;
@@ -1689,6 +1723,7 @@ int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn) {
     np.hscale = float(double(NB8) / np.r2);
     np.max_nn = max_nn;
     np.dense_k = dense_k(max_nn, np.r2);
+    np.preclass = normals_preclass();
     hipEvent_t ev;
     ctx->tic("fpfh", &ev);
     nbr_lists_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_idx, d_d2, d_cnt,

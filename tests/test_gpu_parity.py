@@ -105,6 +105,27 @@ def test_normals(dev, seq8k, seq64k, which):
         _release(dev, ids)
 
 
+@pytest.mark.parametrize("max_nn", [300, 100, 30])
+def test_normals_preclassification_bit_identical(dev, seq64k, max_nn, monkeypatch):
+    """The kNN truncation's final pass settles most points with the f32 distance against the
+    selection state's thresholds (2e-6 relative margin) and leaves only a band to the exact f64
+    classification. That may never change a neighbourhood: normals must be bit-identical to
+    LSM_NORMALS_EXACT=1 (every point through the f64 test), also under heavier truncation."""
+    ids = [dev.upload(s) for s in seq64k.scans]
+    try:
+        prm = _lib.prep_params(max_nn=max_nn)
+        dev.preprocess(ids, prm)
+        fast = [dev.download(i, normals=True)[1] for i in ids]
+        monkeypatch.setenv("LSM_NORMALS_EXACT", "1")
+        dev.preprocess(ids, prm)
+        monkeypatch.delenv("LSM_NORMALS_EXACT")
+        exact = [dev.download(i, normals=True)[1] for i in ids]
+        for a, b in zip(fast, exact):
+            assert np.array_equal(a, b)
+    finally:
+        _release(dev, ids)
+
+
 def test_normals_degenerate_neighbourhoods(dev):
     """kNN-300 truncation on pathological neighbourhoods: 400 exact duplicates of one point (one
     d2 value holds more than a u8 histogram bin can count and more than the selection buffer
