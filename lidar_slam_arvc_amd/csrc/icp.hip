@@ -786,6 +786,149 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
             if (fs[c]) atomicAdd(fstats + c, (unsigned long long)fs[c]);
 }
 
+// nn_fallback with GL lanes per query (64 / GL queries per wave): the same shells, block bounds
+// and stop test as nn_fallback, each group of GL aligned lanes running one query's search (a
+// first-shell survivor block holds ~14 points, so 16 lanes scan it in one step like 64 do).
+// The first shell's 5 x 5 x 5 blocks are decoded with constant divisors.
+template <int GL>
+__device__ __forceinline__ void group_top2(Top2 &t) {
+#pragma unroll
+    for (int off = GL / 2; off > 0; off >>= 1) {
+        const float od = __shfl_xor(t.bd2, off, LSM_WAVE);
+        const int oi = __shfl_xor(t.bidx, off, LSM_WAVE);
+        const float os = __shfl_xor(t.sd2, off, LSM_WAVE);
+        if (oi == t.bidx) {
+            t.sd2 = fminf(t.sd2, os);
+        } else if (better(od, oi, t.bd2, t.bidx)) {
+            t.sd2 = fminf(os, t.bd2);
+            t.bd2 = od;
+            t.bidx = oi;
+        } else {
+            t.sd2 = fminf(t.sd2, od);
+        }
+    }
+    t.lim = prune2(t.bd2, t.sd2, t.m);
+}
+
+template <int GL>
+__global__ void __launch_bounds__(LSM_WAVE)
+nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
+              const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
+              uint32_t queue_cap, int32_t *__restrict__ corr, float *__restrict__ rho,
+              unsigned long long *__restrict__ fstats = nullptr) {
+    constexpr int NG = LSM_WAVE / GL;
+    const int lane = threadIdx.x, sub = lane & (GL - 1), grp = lane / GL;
+    const uint64_t gmask = (GL == 64 ? ~0ull : ((1ull << GL) - 1ull)) << (grp * GL);
+    const uint32_t total = min(*queue_n, queue_cap);
+    uint32_t fs[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t base = blockIdx.x * NG; base < total; base += gridDim.x * NG) {
+        const uint32_t it = base + uint32_t(grp);
+        if (it >= total) continue;   // whole groups only: the group below stays converged
+        if (sub == 0) fs[0] += 1;
+        const FallbackItem q = queue[it];
+        const PairState &P = st[q.pair];
+        const CloudDev S = cds[P.src];
+        const CloudDev G = cds[P.tgt];
+        double qx64, qy64, qz64;
+        transform_point(P.T, lsm_ld(S.xyz, q.i), qx64, qy64, qz64);
+        const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
+        Top2 t2 = top2_init(q.best, q.best_d2, q.second_d2, q.margin);
+        const float B = G.cell * float(LSM_BLK);
+        const float gx1 = G.ox + G.nx * G.cell, gy1 = G.oy + G.ny * G.cell,
+                    gz1 = G.oz + G.nz * G.cell;
+        const float box2 = gap2(qx, G.ox, gx1) + gap2(qy, G.oy, gy1) + gap2(qz, G.oz, gz1);
+        float fbound = 0.f;
+        if (G.n <= 0) {
+            fbound = INFINITY;
+        } else if (box2 >= prm.maxc2) {
+            fbound = sqrtf(box2);
+            if (sub == 0) fs[6] += 1;
+        } else {
+            const float invB = 1.f / B;
+            const int qbx = (int)floorf((qx - G.ox) * invB), qby = (int)floorf((qy - G.oy) * invB),
+                      qbz = (int)floorf((qz - G.oz) * invB);
+            auto outside = [](int v, int n) { return v < 0 ? -v : (v > n - 1 ? v - (n - 1) : 0); };
+            const int r0 = max(outside(qbx, G.nbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
+            const uint32_t *cs = G.cell_start;
+            int ra = r0, rb = r0 == 0 ? FB_R0 : r0;
+            for (;;) {
+                if (sub == 0) fs[1] += 1;
+                const bool cube = ra == 0;   // rings 0 .. FB_R0 as one (2 FB_R0 + 1)^3 cube
+                const int nitems = ring_prefix(rb + 1) - ring_prefix(ra);
+                for (int b0 = 0; b0 < nitems; b0 += GL) {
+                    if (sub == 0) fs[2] += 1;
+                    const int t = b0 + sub;
+                    uint32_t a = 0, b = 0;
+                    if (t < nitems) {
+                        int dx, dy, dz;
+                        if (cube) {
+                            constexpr int W = 2 * FB_R0 + 1;
+                            dz = t / (W * W) - FB_R0;
+                            const int u = t % (W * W);
+                            dy = u / W - FB_R0;
+                            dx = u % W - FB_R0;
+                        } else {
+                            int r = ra, u = t;
+                            while (u >= ring_size(r)) u -= ring_size(r++);
+                            ring_offset(r, u, dx, dy, dz);
+                        }
+                        const int bx = qbx + dx, by = qby + dy, bz = qbz + dz;
+                        if (bx >= 0 && bx < G.nbx && by >= 0 && by < G.nby && bz >= 0 &&
+                            bz < G.nbz) {
+                            const float lb2 = gap2(qx, G.ox + bx * B, G.ox + (bx + 1) * B) +
+                                              gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
+                                              gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
+                            if (lb2 * 0.9999f < t2.lim) {
+                                const int bid = (bz * G.nby + by) * G.nbx + bx;
+                                a = lsm_ld(cs, size_t(bid) * LSM_BLK_CELLS);
+                                b = lsm_ld(cs, size_t(bid + 1) * LSM_BLK_CELLS);
+                            }
+                        }
+                    }
+                    uint64_t mask = __ballot(b > a) & gmask;
+                    while (mask) {
+                        const int src = __ffsll((unsigned long long)mask) - 1;
+                        mask &= mask - 1;
+                        const uint32_t ra_ = __shfl(a, src, LSM_WAVE), rb_ = __shfl(b, src, LSM_WAVE);
+                        if (sub == 0) {
+                            fs[3] += 1;
+                            fs[4] += rb_ - ra_;
+                        }
+                        for (uint32_t k = ra_ + uint32_t(sub); k < rb_; k += GL)
+                            top2_add(sqd(lsm_ld(G.xyz, k), qx, qy, qz), int(k), t2);
+                    }
+                }
+                group_top2<GL>(t2);
+                const int r = rb;
+                float bound = INFINITY;
+                if (qbx - r > 0) bound = fminf(bound, qx - (G.ox + (qbx - r) * B));
+                if (qbx + r + 1 < G.nbx) bound = fminf(bound, G.ox + (qbx + r + 1) * B - qx);
+                if (qby - r > 0) bound = fminf(bound, qy - (G.oy + (qby - r) * B));
+                if (qby + r + 1 < G.nby) bound = fminf(bound, G.oy + (qby + r + 1) * B - qy);
+                if (qbz - r > 0) bound = fminf(bound, qz - (G.oz + (qbz - r) * B));
+                if (qbz + r + 1 < G.nbz) bound = fminf(bound, G.oz + (qbz + r + 1) * B - qz);
+                if (bound == INFINITY || t2.bd2 <= bound * bound * 0.99999f ||
+                    bound >= prm.maxc || rb >= 4095) {
+                    fbound = bound;
+                    break;
+                }
+                ra = rb + 1;
+                rb = ra;
+            }
+        }
+        if (sub == 0) {
+            const int64_t g = P.src_off + q.i;
+            const bool hit = t2.bidx >= 0 && t2.bd2 < prm.maxc2;
+            fs[5] += hit ? 1 : 0;
+            corr[g] = hit ? t2.bidx : -1;
+            rho[g] = hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound);
+        }
+    }
+    if (fstats && sub == 0)
+        for (int c = 0; c < 7; ++c)
+            if (fs[c]) atomicAdd(fstats + c, (unsigned long long)fs[c]);
+}
+
 // ------------------------------------------------------------------------------------------
 // residual / Jacobian accumulation (deterministic block partials)
 // ------------------------------------------------------------------------------------------
@@ -1242,6 +1385,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
     } ev_return{ctx, pass_ev, passes};
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
+    static const int FB_LANES = int(envf("LSM_NN_FB", 32));   // lanes per fallback query
     static const int PASS_LAG = [] {   // passes queued ahead of the last one read back
         const char *e = getenv("LSM_PASS_LAG");
         return e ? std::max(1, atoi(e)) : 2;
@@ -1299,9 +1443,19 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                                                          d_qn + pass, qcap, d_sqn + pass);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
-        nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(
-            d_ps, d_cd, prm, d_q, d_qn + pass, qcap, d_corr, d_rho,
-            d_nst ? d_nst + size_t(ncnt) * NN_NSTAT + size_t(pass) * 8 : nullptr);
+        {
+            unsigned long long *fst = d_nst ? d_nst + size_t(ncnt) * NN_NSTAT + size_t(pass) * 8
+                                            : nullptr;
+            if (FB_LANES == 16)
+                nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                qcap, d_corr, d_rho, fst);
+            else if (FB_LANES == 32)
+                nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                qcap, d_corr, d_rho, fst);
+            else
+                nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass, qcap,
+                                                          d_corr, d_rho, fst);
+        }
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);
         if (p.method == LSM_P2PLANE)

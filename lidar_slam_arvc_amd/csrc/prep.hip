@@ -669,6 +669,23 @@ __device__ __forceinline__ int sel_classify(const Sel &S, double d2, uint32_t k)
     return b < S.b ? -1 : (b > S.b ? 1 : 0);
 }
 
+// f32 thresholds of the classification: a point whose f32 d2 (within 4.2e-7 relative of the
+// exact one; 2e-6 of margin) lies below `below32` is certainly "below" (and inside the ball), one
+// above `above32` certainly "above". sel_classify: below iff d2 < dlo or (d2 <= dhi and bin < b),
+// above iff d2 > dhi or (d2 >= dlo and bin > b); the bins of a d2 level are monotone in d2 with
+// edges lo + j / scale. np.preclass = 0 disables both (every point takes the f64 test).
+__device__ __forceinline__ void sel_thresholds(const Sel &S, const NormalParams &np,
+                                               float &below32, float &above32) {
+    double lo_t = S.dlo, hi_t = S.dhi;
+    if (!S.by_idx && S.scale > 0.0) {   // (scale 0: one bin holding every point)
+        lo_t = fmax(lo_t, fmin(S.dhi, S.lo + double(S.b) / S.scale));
+        if (S.b < S.nb - 1) hi_t = fmin(hi_t, fmax(S.dlo, S.lo + double(S.b + 1) / S.scale));
+    }
+    lo_t = fmin(lo_t, np.r2);   // below also needs d2 < r2
+    below32 = np.preclass && lo_t > 0.0 ? float(lo_t * (1.0 - 2e-6)) : -1.f;
+    above32 = np.preclass && hi_t < 1e30 ? float(hi_t * (1.0 + 2e-6)) : INFINITY;
+}
+
 // fire-and-forget LDS add (ds_add_u32: no read-back, so the walk does not wait on LDS)
 __device__ __forceinline__ void lds_add(uint32_t *a, uint32_t v) {
     __hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -869,16 +886,8 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // d2 below min(r2, dlo, the chosen d2 bin's lower edge) is certainly "below", d2 above
     // max(dhi-side bounds) certainly "above"; only the band between takes the exact f64 test
     // (the f32 d2 is within 4.2e-7 relative; 2e-6 of margin).
-    // (sel_classify: below iff d2 < dlo or, d2 <= dhi, bin < b; above iff d2 > dhi or, d2 >= dlo,
-    // bin > b -- the bins of d2 levels are monotone in d2 with edges lo + j / scale)
-    double lo_t = S.dlo, hi_t = S.dhi;
-    if (!S.by_idx) {
-        lo_t = fmax(lo_t, fmin(S.dhi, S.lo + double(S.b) / S.scale));
-        if (S.b < S.nb - 1) hi_t = fmin(hi_t, fmax(S.dlo, S.lo + double(S.b + 1) / S.scale));
-    }
-    lo_t = fmin(lo_t, np.r2);   // below also needs d2 < r2
-    const float below32 = np.preclass && lo_t > 0.0 ? float(lo_t * (1.0 - 2e-6)) : -1.f;
-    const float above32 = np.preclass && hi_t < 1e30 ? float(hi_t * (1.0 + 2e-6)) : INFINITY;
+    float below32, above32;
+    sel_thresholds(S, np, below32, above32);
     uint32_t m = 0;
     ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
