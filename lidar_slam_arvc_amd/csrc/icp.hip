@@ -117,9 +117,14 @@ __device__ __forceinline__ void top2_add(float d2, int k, Top2 &b) {
     b.lim = prune2(b.bd2, b.sd2, b.m);
 }
 
+// The f32 squared distance that ranks candidates: ONE fixed rounding sequence (explicit fmas,
+// no compiler contraction), so every search path -- box search, walks in either direction,
+// fallback, warm start, certificate -- computes bit-identical values and exact (d2, index) ties
+// resolve the same way everywhere (hipcc contracts a * b + c per call site otherwise).
 __device__ __forceinline__ float sqd(const float4 t, float qx, float qy, float qz) {
+#pragma clang fp contract(off)
     const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
-    return dx * dx + dy * dy + dz * dz;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
 }
 
 // One x-sorted run [a, b) of a cell row whose slab is at least dyz2 (squared, underestimated)
