@@ -279,7 +279,10 @@ def main():
         tfile = os.path.join(ROOT, "profiles", "nn_traffic.json")
         if os.path.exists(tfile) and not (ouster or loop):
             with open(tfile) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                tj = json.load(f)
+            # PMC traffic of the same workload (profiles/nn_traffic.json, tools/pmc_nn.sh)
+            if tj.get("pairs_per_gpu") == P:
+                traffic = tj.get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": "correspondence pass: nn_kernel (stability check + box search) + "

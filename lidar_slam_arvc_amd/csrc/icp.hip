@@ -51,12 +51,13 @@ struct NNParams {
 
 // Correspondence state of one source point, carried from pass to pass (SoA arrays):
 //   corr[i]  nearest target point (sorted index), -1 = none within max_corr
-//   rho[i]   a lower bound on the distance from the pass's f32 query point q_i to every target
-//            point OTHER than corr[i] (to every point when corr[i] = -1), metres.
-// Stability certificate: if q_i moves by delta between passes and |q_i - t_corr| + delta < rho,
-// no other point can have come nearer than t_corr, so the nearest neighbour is unchanged and
-// needs no search (rho <- rho - delta). Later ICP passes move the source by micrometres to
-// millimetres, so nearly every query of a converging pair is certified with two loads.
+//   cert[i]  (q_s, rho): the f32 query point of the search that found corr[i], and a lower
+//            bound rho on the distance from q_s to every target point OTHER than corr[i] (to
+//            every point when corr[i] = -1), metres.
+// Stability certificate: if the query now sits at q with D = |q - q_s| and |q - t_corr| + D <
+// rho, no other point can be nearer than t_corr, so the nearest neighbour is unchanged and needs
+// no search (and nothing is written). Later ICP passes move the source by micrometres to
+// millimetres, so nearly every query of a converging pair is certified with three loads.
 struct FallbackItem {
     int32_t pair;
     int32_t i;        // source point (sorted order)
@@ -360,12 +361,13 @@ __device__ __forceinline__ void group_top2(Top2 &t, int L) {
 // iterating) is not left to one lane. Every lane of the group returns the same values.
 __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, const CloudDev &G,
                                          int i, int prev, float m, const NNParams &prm,
-                                         int &result, float &rho, Top2 &t2, int sub = 0,
-                                         int L = 1, NNStat *ns = nullptr) {
+                                         int &result, float &rho, Top2 &t2, float4 &qp,
+                                         int sub = 0, int L = 1, NNStat *ns = nullptr) {
     NN_ST(ns, 0, 1);
     double qx64, qy64, qz64;
     transform_point(T, lsm_ld(S.xyz, i), qx64, qy64, qz64);
     const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
+    qp = make_float4(qx, qy, qz, 0.f);
     t2 = top2_init(-1, INFINITY, INFINITY, m);
     result = -1;
     rho = INFINITY;
@@ -470,48 +472,51 @@ __device__ __forceinline__ void push_fallback(bool pending, int pair, int i, flo
     }
 }
 
-// Stability check of one query (passes >= 1). delta = |q - q'| between this pass's and the
-// previous pass's f32 query points (both recomputed from the stored transforms, f64 difference
-// of f32 values). Certified: |q - t_corr| (1 + 1e-5) + delta < rho, i.e. every other point is
-// strictly farther even after the f32 rounding of the search's squared distances (relative
-// error < 1e-6); the neighbour stays (or drops out when it left max_corr) and rho shrinks by
-// delta, rounded down. A query without a neighbour stays without one while
-// rho - delta >= max_corr (1 + 1e-5). Returns false when the query must be searched; `m` is
-// then its margin for the search's rho.
+// Stability check of one query (passes >= 1). cert[g] = (q_s, rho): the f32 query point of the
+// search that found corr[g] and that search's rho (a lower bound on |q_s - t'| for every target
+// point t' other than corr[g]; for every point when corr[g] = -1). For this pass's query point
+// q, every other point is at least rho - D away, D = |q - q_s| (triangle inequality, f64 of the
+// f32 points, rounded up). Certified: |q - t_corr| (1 + 1e-5) + D < rho, i.e. every other point
+// is strictly farther even after the f32 rounding of the search's squared distances (relative
+// error < 1e-6); nothing is written (cert keeps the search's reference point). D is the direct
+// displacement since the search, not a sum of per-pass steps, so a pair that oscillates keeps
+// its certificates. A query without a neighbour stays without one while rho - D >= max_corr
+// (1 + 1e-5); one whose neighbour left max_corr drops it and is re-based at q. Returns false
+// when the query must be searched; `m` is then its margin for the search's rho.
+__device__ __forceinline__ float motion_margin(const PairState &P, const float4 s,
+                                               const NNParams &prm);
+
 __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &S,
                                            const CloudDev &G, int i, int64_t g,
                                            const NNParams &prm, int32_t *__restrict__ corr,
-                                           float *__restrict__ rho, float &m) {
+                                           float4 *__restrict__ cert, float &m) {
     const float4 s = lsm_ld(S.xyz, i);
-    double x, y, z, xp, yp, zp;
+    double x, y, z;
     transform_point(P.T, s, x, y, z);
-    transform_point(P.Tp, s, xp, yp, zp);
     const float qx = float(x), qy = float(y), qz = float(z);
-    const double ddx = double(qx) - double(float(xp)), ddy = double(qy) - double(float(yp)),
-                 ddz = double(qz) - double(float(zp));
-    const double dq = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
-    const double delta = dq * (1.0 + 1e-6) + 1e-7;
-    m = float(prm.m_mul * dq + prm.m_add);
+    const float4 c = lsm_ld(cert, g);
+    const double ddx = double(qx) - double(c.x), ddy = double(qy) - double(c.y),
+                 ddz = double(qz) - double(c.z);
+    const double delta = sqrt(ddx * ddx + ddy * ddy + ddz * ddz) * (1.0 + 1e-6) + 1e-7;
     const int prev = corr[g];
-    const double r = double(rho[g]);
+    const double r = double(c.w);
     if (prev >= 0) {
         const float4 t = lsm_ld(G.xyz, prev);
         const double ex = double(qx) - double(t.x), ey = double(qy) - double(t.y),
                      ez = double(qz) - double(t.z);
         const double e = sqrt(ex * ex + ey * ey + ez * ez);
-        if (!(e * (1.0 + 1e-5) + delta < r)) return false;
-        if (sqd(t, qx, qy, qz) < prm.maxc2) {
-            rho[g] = __double2float_rd(r - delta);
-        } else {   // the neighbour left max_corr: no point is within it, none nearer than e
-            corr[g] = -1;
-            rho[g] = __double2float_rd(fmin(e * (1.0 - 1e-5), r - delta));
+        if (e * (1.0 + 1e-5) + delta < r) {
+            if (sqd(t, qx, qy, qz) >= prm.maxc2) {
+                // the neighbour left max_corr: no point is within it, none nearer than e
+                corr[g] = -1;
+                cert[g] = make_float4(qx, qy, qz, __double2float_rd(fmin(e * (1.0 - 1e-5), r - delta)));
+            }
+            return true;
         }
+    } else if (prev == -1 && r - delta >= double(prm.maxc) * (1.0 + 1e-5)) {
         return true;
     }
-    if (prev == -1 && r - delta >= double(prm.maxc) * (1.0 + 1e-5)) {
-        rho[g] = __double2float_rd(r - delta);
-        return true;
-    }
+    m = motion_margin(P, s, prm);
     return false;
 }
 
@@ -539,7 +544,7 @@ __device__ __forceinline__ void flush_stats(const NNStat &ls, unsigned long long
 template <bool CHECK, bool STATS = false>
 __global__ void __launch_bounds__(NN_THREADS)
 nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
-          NNParams prm, int32_t *__restrict__ corr, float *__restrict__ rho,
+          NNParams prm, int32_t *__restrict__ corr, float4 *__restrict__ cert,
           FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n, uint32_t queue_cap,
           uint32_t *__restrict__ searched, unsigned long long *__restrict__ stats = nullptr) {
     NNStat ls{};
@@ -564,7 +569,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         __shared__ float s_m[NN_THREADS];
         __shared__ int32_t s_cnt[NN_THREADS / LSM_WAVE];
         bool need = false;
-        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, rho, m);
+        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, cert, m);
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         const uint64_t bm = __ballot(need);
         if (lane == 0) s_cnt[w] = __popcll(bm);
@@ -598,13 +603,14 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         float r = 0.f;
         Top2 t2 = top2_init(-1, INFINITY, INFINITY, m);
         bool pending = false;
+        float4 qp;
         if (live)
-            pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2, sub, L, ns);
+            pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2, qp, sub, L, ns);
         const bool lead = live && sub == 0;
         push_fallback(pending && lead, task.pair, i, m, t2, queue, queue_n, queue_cap);
         if (lead) {
             corr[g] = pending ? -2 : result;
-            rho[g] = r;
+            if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
         }
         if (STATS) {
             if (sub != 0) ls.v[0] = 0;   // one search per query
@@ -620,11 +626,12 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
     if (live && P.iter > 0) m = motion_margin(P, lsm_ld(S.xyz, i), prm);
     Top2 t2 = top2_init(-1, INFINITY, INFINITY, m);
     bool pending = false;
-    if (live) pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2, 0, 1, ns);
+    float4 qp;
+    if (live) pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2, qp, 0, 1, ns);
     push_fallback(pending, task.pair, i, m, t2, queue, queue_n, queue_cap);
     if (live) {
         corr[g] = pending ? -2 : result;
-        rho[g] = r;
+        if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
     }
     if (STATS) flush_stats(ls, stats);
 }
@@ -699,7 +706,7 @@ __device__ __forceinline__ void ring_offset(int r, int t, int &dx, int &dy, int 
 __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
             const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
-            uint32_t queue_cap, int32_t *__restrict__ corr, float *__restrict__ rho,
+            uint32_t queue_cap, int32_t *__restrict__ corr, float4 *__restrict__ cert,
             unsigned long long *__restrict__ fstats = nullptr) {
     const int lane = threadIdx.x;
     const uint32_t total = min(*queue_n, queue_cap);
@@ -798,7 +805,7 @@ nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, 
             const bool hit = t2.bidx >= 0 && t2.bd2 < prm.maxc2;
             fs[5] += hit ? 1 : 0;
             corr[g] = hit ? t2.bidx : -1;
-            rho[g] = hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound);
+            cert[g] = make_float4(qx, qy, qz, hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound));
         }
     }
     if (fstats && lane == 0)
@@ -834,7 +841,7 @@ template <int GL>
 __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
               const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
-              uint32_t queue_cap, int32_t *__restrict__ corr, float *__restrict__ rho,
+              uint32_t queue_cap, int32_t *__restrict__ corr, float4 *__restrict__ cert,
               unsigned long long *__restrict__ fstats = nullptr) {
     constexpr int NG = LSM_WAVE / GL;
     const int lane = threadIdx.x, sub = lane & (GL - 1), grp = lane / GL;
@@ -941,7 +948,7 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
             const bool hit = t2.bidx >= 0 && t2.bd2 < prm.maxc2;
             fs[5] += hit ? 1 : 0;
             corr[g] = hit ? t2.bidx : -1;
-            rho[g] = hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound);
+            cert[g] = make_float4(qx, qy, qz, hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound));
         }
     }
     if (fstats && sub == 0)
@@ -1322,7 +1329,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     if ((rc = upload(ctx, "i_pbytes", pbytes, &d_pbytes))) return rc;
     const size_t nsrc_tot = size_t(std::max<int64_t>(src_off, 1));
     int32_t *d_corr = (int32_t *)ctx->buf("i_corr", nsrc_tot * 4);
-    float *d_rho = (float *)ctx->buf("i_rho", nsrc_tot * 4);
+    float4 *d_cert = (float4 *)ctx->buf("i_cert", nsrc_tot * 16);
     const uint32_t qcap = uint32_t(nsrc_tot);
     FallbackItem *d_q = (FallbackItem *)ctx->buf("i_queue", size_t(qcap) * sizeof(FallbackItem));
     double *d_part = (double *)ctx->buf("i_part", size_t(std::max(slot, 1)) * LSM_ACC * 8);
@@ -1334,7 +1341,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
     int32_t *d_err = (int32_t *)ctx->buf("i_err", 4);
-    if (!d_corr || !d_rho || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
+    if (!d_corr || !d_cert || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
         !d_plan || !d_flags || !d_err) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
@@ -1455,15 +1462,15 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             unsigned long long *sp = d_nst + size_t(pass) * NN_NSTAT;
             if (pass < CERT_FROM || nocert)
                 nn_kernel<false, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_rho, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+                    tp, d_ps, d_cd, prm, d_corr, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
             else
                 nn_kernel<true, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_rho, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+                    tp, d_ps, d_cd, prm, d_corr, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
         } else if (pass < CERT_FROM || nocert)
-            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_rho, d_q,
+            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_cert, d_q,
                                                           d_qn + pass, qcap, d_sqn + pass);
         else
-            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_rho, d_q,
+            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_cert, d_q,
                                                          d_qn + pass, qcap, d_sqn + pass);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
@@ -1472,13 +1479,13 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                                             : nullptr;
             if (FB_LANES == 16)
                 nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_rho, fst);
+                                                                qcap, d_corr, d_cert, fst);
             else if (FB_LANES == 32)
                 nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_rho, fst);
+                                                                qcap, d_corr, d_cert, fst);
             else
                 nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass, qcap,
-                                                          d_corr, d_rho, fst);
+                                                          d_corr, d_cert, fst);
         }
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);

@@ -40,8 +40,9 @@ hbm = (2.0 * fetch_kb + write_kb) * 1024.0 / max(passes, 1)
 print(json.dumps({
     "kernel": "correspondence pass (nn_kernel + nn_fallback)",
     "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-              "bench.py --steps 2 --warmup 1 (tools/pmc_nn.sh)",
+              "bench.py --steps 2 --warmup 1, default workload (tools/pmc_nn.sh)",
     "passes": passes, "dispatches": [n1, n2],
+    "pairs_per_gpu": bench["config"].get("pairs_per_gpu") if bench else None,
     "fetch_size_kb_per_pass": fetch_kb / max(passes, 1),
     "write_size_kb_per_pass": write_kb / max(passes2, 1),
     "correction": "gfx950 FETCH_SIZE counts 1/2 of wide coalesced reads: fetch doubled; "
