@@ -8,7 +8,7 @@
 //                      the target's cell grid (own cell, then the 26 neighbours pruned by their
 //                      lower-bound distance). A query whose nearest point is provably inside the
 //                      3x3x3 block is resolved; the rest (a few %) go to a queue.
-//   nn_fallback        one wave per queued query: expanding boxes, the wave strides over each
+//   nn_fallback_g      32 lanes (or a wave) per queued query: expanding boxes, the group strides over each
 //                      cell row, (d2, index) wave-min -> exact nearest within max_corr.
 //   accumulate         one lane per source point: f64 residual / Jacobian of the correspondence,
 //                      fixed-tree wave + LDS reduction into per-block partials (deterministic).
@@ -639,26 +639,6 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
 // ------------------------------------------------------------------------------------------
 // exact fallback: one wave per unresolved query, expanding boxes (shells)
 // ------------------------------------------------------------------------------------------
-// (nearest, second) wave reduction; lanes holding the same point merge their second distances
-__device__ __forceinline__ void wave_top2(Top2 &t) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float od = __shfl_xor(t.bd2, off, LSM_WAVE);
-        const int oi = __shfl_xor(t.bidx, off, LSM_WAVE);
-        const float os = __shfl_xor(t.sd2, off, LSM_WAVE);
-        if (oi == t.bidx) {
-            t.sd2 = fminf(t.sd2, os);
-        } else if (better(od, oi, t.bd2, t.bidx)) {
-            t.sd2 = fminf(os, t.bd2);
-            t.bd2 = od;
-            t.bidx = oi;
-        } else {
-            t.sd2 = fminf(t.sd2, od);
-        }
-    }
-    t.lim = prune2(t.bd2, t.sd2, t.m);
-}
-
 __device__ __forceinline__ float gap2(float q, float lo, float hi) {
     const float d = q < lo ? lo - q : (q > hi ? q - hi : 0.f);
     return d * d;
@@ -698,125 +678,14 @@ __device__ __forceinline__ void ring_offset(int r, int t, int &dx, int &dy, int 
     dy = u % n2 - r + 1;
 }
 
-// Exact 1-NN for the queries the box search could not resolve: one wave per query walks
-// Chebyshev rings of 4x4x4-cell blocks (each block one contiguous point range) outward from the
-// query's block. Lanes test 64 blocks at a time against the current pruning radius
-// (prune2, lower-bound pruning); the surviving blocks are scanned by the whole wave. Stops when
-// every unscanned point is provably farther than the best, or than max_corr.
-__global__ void __launch_bounds__(LSM_WAVE)
-nn_fallback(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
-            const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
-            uint32_t queue_cap, int32_t *__restrict__ corr, float4 *__restrict__ cert,
-            unsigned long long *__restrict__ fstats = nullptr) {
-    const int lane = threadIdx.x;
-    const uint32_t total = min(*queue_n, queue_cap);
-    // statistics (LSM_NN_STATS): queries, rings, chunks, blocks scanned, points, hits, outside
-    uint32_t fs[7] = {0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
-        fs[0] += 1;
-        const FallbackItem q = queue[it];
-        const PairState &P = st[q.pair];
-        const CloudDev S = cds[P.src];
-        const CloudDev G = cds[P.tgt];
-        double qx64, qy64, qz64;
-        transform_point(P.T, lsm_ld(S.xyz, q.i), qx64, qy64, qz64);
-        const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
-        Top2 t2 = top2_init(q.best, q.best_d2, q.second_d2, q.margin);
-        const float B = G.cell * float(LSM_BLK);
-        const float gx1 = G.ox + G.nx * G.cell, gy1 = G.oy + G.ny * G.cell,
-                    gz1 = G.oz + G.nz * G.cell;
-        const float box2 = gap2(qx, G.ox, gx1) + gap2(qy, G.oy, gy1) + gap2(qz, G.oz, gz1);
-        float fbound = 0.f;   // every unscanned point is at least this far (0: unknown)
-        if (G.n <= 0) {
-            fbound = INFINITY;
-        } else if (box2 >= prm.maxc2) {
-            fbound = sqrtf(box2);   // nothing within max_corr: every point is outside the box
-            fs[6] += 1;
-        } else {
-            const float invB = 1.f / B;
-            const int qbx = (int)floorf((qx - G.ox) * invB), qby = (int)floorf((qy - G.oy) * invB),
-                      qbz = (int)floorf((qz - G.oz) * invB);
-            auto outside = [](int v, int n) { return v < 0 ? -v : (v > n - 1 ? v - (n - 1) : 0); };
-            const int r0 = max(outside(qbx, G.nbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
-            const uint32_t *cs = G.cell_start;
-            // shells of rings [ra, rb]: the first one (query inside the grid) covers rings
-            // 0 .. FB_R0 at once -- 125 blocks in two chunks, one merge and stop test -- and the
-            // rest are single rings. Lanes keep their own (nearest, second) across a shell's
-            // chunks (their pruning radii are only looser than the wave's); the shell ends with
-            // the wave merge and the stop test.
-            int ra = r0, rb = r0 == 0 ? FB_R0 : r0;
-            for (;;) {
-                fs[1] += 1;
-                const int nitems = ring_prefix(rb + 1) - ring_prefix(ra);
-                for (int base = 0; base < nitems; base += LSM_WAVE) {
-                    fs[2] += 1;
-                    const int t = base + lane;
-                    uint32_t a = 0, b = 0;
-                    if (t < nitems) {
-                        int r = ra, u = t;
-                        while (u >= ring_size(r)) u -= ring_size(r++);
-                        int dx, dy, dz;
-                        ring_offset(r, u, dx, dy, dz);
-                        const int bx = qbx + dx, by = qby + dy, bz = qbz + dz;
-                        if (bx >= 0 && bx < G.nbx && by >= 0 && by < G.nby && bz >= 0 &&
-                            bz < G.nbz) {
-                            const float lb2 = gap2(qx, G.ox + bx * B, G.ox + (bx + 1) * B) +
-                                              gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
-                                              gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
-                            if (lb2 * 0.9999f < t2.lim) {
-                                const int bid = (bz * G.nby + by) * G.nbx + bx;
-                                a = lsm_ld(cs, size_t(bid) * LSM_BLK_CELLS);
-                                b = lsm_ld(cs, size_t(bid + 1) * LSM_BLK_CELLS);
-                            }
-                        }
-                    }
-                    uint64_t mask = __ballot(b > a);
-                    while (mask) {
-                        const int src = __ffsll((unsigned long long)mask) - 1;
-                        mask &= mask - 1;
-                        const uint32_t ra_ = __shfl(a, src, LSM_WAVE), rb_ = __shfl(b, src, LSM_WAVE);
-                        fs[3] += 1;
-                        fs[4] += rb_ - ra_;
-                        for (uint32_t k = ra_ + lane; k < rb_; k += LSM_WAVE)
-                            top2_add(sqd(lsm_ld(G.xyz, k), qx, qy, qz), int(k), t2);
-                    }
-                }
-                wave_top2(t2);
-                // every unscanned point lies outside the block cube [qb - rb, qb + rb]
-                const int r = rb;
-                float bound = INFINITY;
-                if (qbx - r > 0) bound = fminf(bound, qx - (G.ox + (qbx - r) * B));
-                if (qbx + r + 1 < G.nbx) bound = fminf(bound, G.ox + (qbx + r + 1) * B - qx);
-                if (qby - r > 0) bound = fminf(bound, qy - (G.oy + (qby - r) * B));
-                if (qby + r + 1 < G.nby) bound = fminf(bound, G.oy + (qby + r + 1) * B - qy);
-                if (qbz - r > 0) bound = fminf(bound, qz - (G.oz + (qbz - r) * B));
-                if (qbz + r + 1 < G.nbz) bound = fminf(bound, G.oz + (qbz + r + 1) * B - qz);
-                if (bound == INFINITY || t2.bd2 <= bound * bound * 0.99999f ||
-                    bound >= prm.maxc || rb >= 4095) {
-                    fbound = bound;
-                    break;
-                }
-                ra = rb + 1;
-                rb = ra;
-            }
-        }
-        if (lane == 0) {
-            const int64_t g = P.src_off + q.i;
-            const bool hit = t2.bidx >= 0 && t2.bd2 < prm.maxc2;
-            fs[5] += hit ? 1 : 0;
-            corr[g] = hit ? t2.bidx : -1;
-            cert[g] = make_float4(qx, qy, qz, hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound));
-        }
-    }
-    if (fstats && lane == 0)
-        for (int c = 0; c < 7; ++c)
-            if (fs[c]) atomicAdd(fstats + c, (unsigned long long)fs[c]);
-}
-
-// nn_fallback with GL lanes per query (64 / GL queries per wave): the same shells, block bounds
-// and stop test as nn_fallback, each group of GL aligned lanes running one query's search (a
-// first-shell survivor block holds ~14 points, so 16 lanes scan it in one step like 64 do).
-// The first shell's 5 x 5 x 5 blocks are decoded with constant divisors.
+// Exact 1-NN for the queries the box search could not resolve: a group of GL aligned lanes per
+// query (64 / GL queries per wave) walks Chebyshev rings of 4x4x4-cell blocks (each block one
+// contiguous point range) outward from the query's block. Lanes test GL blocks at a time against
+// the current pruning radius (prune2, lower-bound pruning); the surviving blocks are scanned by
+// the whole group. Stops when every unscanned point is provably farther than the best, or than
+// max_corr. The first shell (rings 0 .. FB_R0, one merge and stop test) is decoded with constant
+// divisors. A first-shell survivor block holds ~14 points, so 32 lanes scan it in one step like
+// 64 do; queries expected to need wide rings take a whole wave (the `far` split).
 template <int GL>
 __device__ __forceinline__ void group_top2(Top2 &t) {
 #pragma unroll
@@ -842,7 +711,9 @@ __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
               const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
               uint32_t queue_cap, int32_t *__restrict__ corr, float4 *__restrict__ cert,
-              unsigned long long *__restrict__ fstats = nullptr) {
+              unsigned long long *__restrict__ fstats, float far2, int far) {
+    // far = 0: the items whose box-search best is within sqrt(far2) (or all when far2 = inf);
+    // far = 1: the others (expected to need wider rings: more lanes per query)
     constexpr int NG = LSM_WAVE / GL;
     const int lane = threadIdx.x, sub = lane & (GL - 1), grp = lane / GL;
     const uint64_t gmask = (GL == 64 ? ~0ull : ((1ull << GL) - 1ull)) << (grp * GL);
@@ -851,8 +722,9 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
     for (uint32_t base = blockIdx.x * NG; base < total; base += gridDim.x * NG) {
         const uint32_t it = base + uint32_t(grp);
         if (it >= total) continue;   // whole groups only: the group below stays converged
-        if (sub == 0) fs[0] += 1;
         const FallbackItem q = queue[it];
+        if ((q.best_d2 > far2) != (far != 0)) continue;
+        if (sub == 0) fs[0] += 1;
         const PairState &P = st[q.pair];
         const CloudDev S = cds[P.src];
         const CloudDev G = cds[P.tgt];
@@ -1412,7 +1284,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
     } ev_return{ctx, pass_ev, passes};
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
-    static const int FB_LANES = int(envf("LSM_NN_FB", 32));   // lanes per fallback query
+    static const int FB_LANES = int(envf("LSM_NN_FB", 32));   // lanes per (near) fallback query
+    static const double FB_FAR = envf("LSM_NN_FB_FAR", 0.0);   // m; 0: one kernel for all items
     static const int PASS_LAG = [] {   // passes queued ahead of the last one read back
         const char *e = getenv("LSM_PASS_LAG");
         return e ? std::max(1, atoi(e)) : 2;
@@ -1477,15 +1350,21 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         {
             unsigned long long *fst = d_nst ? d_nst + size_t(ncnt) * NN_NSTAT + size_t(pass) * 8
                                             : nullptr;
+            // near items (box-search best within FB_FAR metres) with FB_LANES lanes each, the
+            // rest with a whole wave each (wide rings); every item is taken by exactly one
+            const float far2 = FB_FAR > 0.0 ? float(FB_FAR * FB_FAR) : INFINITY;
             if (FB_LANES == 16)
                 nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst);
+                                                                qcap, d_corr, d_cert, fst, far2, 0);
             else if (FB_LANES == 32)
                 nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst);
+                                                                qcap, d_corr, d_cert, fst, far2, 0);
             else
-                nn_fallback<<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass, qcap,
-                                                          d_corr, d_cert, fst);
+                nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                qcap, d_corr, d_cert, fst, far2, 0);
+            if (FB_LANES != 64 && FB_FAR > 0.0)
+                nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                qcap, d_corr, d_cert, fst, far2, 1);
         }
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);
