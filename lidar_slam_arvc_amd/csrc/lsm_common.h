@@ -33,7 +33,7 @@ struct CloudDev {
     const float4 *prior_ref;    // prior normals in reference order (orientation), or nullptr
 };
 
-#define LSM_XYZ_PAD 8      // spare float4 points allocated past every processed cloud's end
+#define LSM_XYZ_PAD 16     // spare float4 points allocated past every processed cloud's end
 #define LSM_BLK 4          // cells per block edge
 #define LSM_BLK_SHIFT 2
 #define LSM_BLK_CELLS 64

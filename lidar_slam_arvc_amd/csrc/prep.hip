@@ -533,7 +533,16 @@ __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, fl
 // points of which ~30 lie left of the window on HDL-64 scans); the walk stops past xh.
 constexpr uint32_t SCAN_BSEARCH = 16;
 constexpr uint32_t SCAN_SLACK = 8;   // scan_run_pred: entry search stops within this many points
-constexpr int NORMALS_G_DEFAULT = 4;
+// points per load group of the normals walks, and whether the next group's loads are issued
+// before the current group is tested (measured per 65 keyframes: G4 6.65 ms, G2 + prefetch 6.43,
+// G4 + prefetch 7.57 -- the extra registers cost occupancy)
+#ifndef LSM_NORMALS_G_DEFAULT
+#define LSM_NORMALS_G_DEFAULT 2
+#endif
+constexpr int NORMALS_G_DEFAULT = LSM_NORMALS_G_DEFAULT;
+#ifndef LSM_NORMALS_PF
+#define LSM_NORMALS_PF 1
+#endif
 
 template <int G, typename Body>
 __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float xl, float xh,
@@ -599,11 +608,28 @@ __device__ __forceinline__ void scan_run_pred(const float4 *xyz, uint32_t a, uin
         }
         a = lo;
     }
+#if LSM_NORMALS_PF
+    // software-pipelined: the next group's loads are in flight while this group is tested (the
+    // loads may run up to 2G - 1 points past the run: within the cloud's LSM_XYZ_PAD spare points)
+    static_assert(2 * G - 1 <= LSM_XYZ_PAD, "prefetched group loads run past a run");
+    if (a >= b) return;
+    float4 nx[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) nx[g] = lsm_ld(xyz, a + uint32_t(g));
+    for (uint32_t k = a; k < b; k += G) {
+        float4 p[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            p[g] = nx[g];
+            nx[g] = lsm_ld(xyz, k + uint32_t(G + g));
+        }
+#else
     static_assert(G <= LSM_XYZ_PAD, "group loads may run LSM_XYZ_PAD points past a run");
     for (uint32_t k = a; k < b; k += G) {
         float4 p[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) p[g] = lsm_ld(xyz, k + uint32_t(g));
+#endif
         bool live = true;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
