@@ -147,9 +147,14 @@ constexpr int NN_NSTAT = 8;
 // than per point); a group may read up to NN_G - 1 points past the walk's stop, never past the
 // run. Short runs (<= lin points) are scanned whole.
 #ifndef LSM_NN_G
-#define LSM_NN_G 4
+#define LSM_NN_G 2
 #endif
 constexpr int NN_G = LSM_NN_G;
+// LSM_NN_PF: software-pipelined walks (scan_run). Measured per 1999-pair step: G 4 104.8 ms,
+// G 2 108.8, G 2 + prefetch 94.3, G 1 / 3 / 4 + prefetch 103.4 / 108.2 / 128.3 (registers)
+#ifndef LSM_NN_PF
+#define LSM_NN_PF 1
+#endif
 
 __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float qx,
                                          float qy, float qz, float dyz2, Top2 &t2, uint32_t lin,
@@ -175,11 +180,29 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
         if (lsm_ld(xs, size_t(mid) * 4) < qx) lo = mid + 1;
         else hi = mid;
     }
-    // rightwards from lo (x >= qx), then leftwards from lo - 1 (x < qx)
+    // rightwards from lo (x >= qx), then leftwards from lo - 1 (x < qx). LSM_NN_PF: the first
+    // groups of both walks are loaded together, and each walk loads its next group before
+    // testing the current one (loads clamped to the run).
+#if LSM_NN_PF
+    float4 r[NN_G], l[NN_G];
+#pragma unroll
+    for (int g = 0; g < NN_G; ++g) {
+        r[g] = lsm_ld(xyz, min(lo + uint32_t(g), b - 1));
+        l[g] = lsm_ld(xyz, uint32_t(max(int(lo) - 1 - g, int(a))));
+    }
+#endif
     for (uint32_t k = lo; k < b; k += NN_G) {
         float4 t[NN_G];
+#if LSM_NN_PF
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) {
+            t[g] = r[g];
+            r[g] = lsm_ld(xyz, min(k + uint32_t(NN_G + g), b - 1));
+        }
+#else
 #pragma unroll
         for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, min(k + uint32_t(g), b - 1));
+#endif
         bool stop = false;
 #pragma unroll
         for (int g = 0; g < NN_G; ++g) {
@@ -197,8 +220,16 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
     }
     for (int k = int(lo) - 1; k >= int(a); k -= NN_G) {
         float4 t[NN_G];
+#if LSM_NN_PF
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) {
+            t[g] = l[g];
+            l[g] = lsm_ld(xyz, uint32_t(max(k - NN_G - g, int(a))));
+        }
+#else
 #pragma unroll
         for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, uint32_t(max(k - g, int(a))));
+#endif
         bool stop = false;
 #pragma unroll
         for (int g = 0; g < NN_G; ++g) {
