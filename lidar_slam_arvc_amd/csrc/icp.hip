@@ -815,17 +815,39 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                             }
                         }
                     }
+                    // survivor blocks one after another; the next block's first points are
+                    // loaded while the current block is tested (a block holds ~14 points, so
+                    // that is usually the whole block)
                     uint64_t mask = __ballot(b > a) & gmask;
-                    while (mask) {
-                        const int src = __ffsll((unsigned long long)mask) - 1;
+                    if (mask) {
+                        int src = __ffsll((unsigned long long)mask) - 1;
                         mask &= mask - 1;
-                        const uint32_t ra_ = __shfl(a, src, LSM_WAVE), rb_ = __shfl(b, src, LSM_WAVE);
-                        if (sub == 0) {
-                            fs[3] += 1;
-                            fs[4] += rb_ - ra_;
+                        uint32_t ra_ = __shfl(a, src, LSM_WAVE), rb_ = __shfl(b, src, LSM_WAVE);
+                        float4 p = lsm_ld(G.xyz, min(ra_ + uint32_t(sub), rb_ - 1));
+                        for (;;) {
+                            const bool more = mask != 0;   // uniform in the group
+                            uint32_t na = 0, nb = 0;
+                            float4 pn = p;
+                            if (more) {
+                                src = __ffsll((unsigned long long)mask) - 1;
+                                mask &= mask - 1;
+                                na = __shfl(a, src, LSM_WAVE);
+                                nb = __shfl(b, src, LSM_WAVE);
+                                pn = lsm_ld(G.xyz, min(na + uint32_t(sub), nb - 1));
+                            }
+                            if (sub == 0) {
+                                fs[3] += 1;
+                                fs[4] += rb_ - ra_;
+                            }
+                            if (ra_ + uint32_t(sub) < rb_)
+                                top2_add(sqd(p, qx, qy, qz), int(ra_ + uint32_t(sub)), t2);
+                            for (uint32_t k = ra_ + uint32_t(sub + GL); k < rb_; k += GL)
+                                top2_add(sqd(lsm_ld(G.xyz, k), qx, qy, qz), int(k), t2);
+                            if (!more) break;
+                            ra_ = na;
+                            rb_ = nb;
+                            p = pn;
                         }
-                        for (uint32_t k = ra_ + uint32_t(sub); k < rb_; k += GL)
-                            top2_add(sqd(lsm_ld(G.xyz, k), qx, qy, qz), int(k), t2);
                     }
                 }
                 group_top2<GL>(t2);
