@@ -1337,8 +1337,9 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
     } ev_return{ctx, pass_ev, passes};
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
-    static const int FB_LANES = int(envf("LSM_NN_FB", 32));   // lanes per (near) fallback query
-    static const double FB_FAR = envf("LSM_NN_FB_FAR", 0.0);   // m; 0: one kernel for all items
+    // search-path knobs are read per call (the tests switch them to prove every path exact)
+    const int FB_LANES = int(envf("LSM_NN_FB", 32));   // lanes per (near) fallback query
+    const double FB_FAR = envf("LSM_NN_FB_FAR", 0.0);   // m; 0: one kernel for all items
     static const int PASS_LAG = [] {   // passes queued ahead of the last one read back
         const char *e = getenv("LSM_PASS_LAG");
         return e ? std::max(1, atoi(e)) : 2;
@@ -1348,7 +1349,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     // passes before CERT_FROM search every query without the stability check: pass 1 follows
     // the first update, which moves the scans by centimetres to decimetres -- beyond nearly
     // every certificate -- so the check would only add its loads before the search
-    static const int CERT_FROM = std::max(1, int(envf("LSM_NN_CERT_FROM", 2)));
+    const int CERT_FROM = std::max(1, int(envf("LSM_NN_CERT_FROM", 2)));
     const char *nc_env = getenv("LSM_NN_NOCERT");
     const bool nocert = nc_env && atoi(nc_env) != 0;
     double ms0 = 0.0;

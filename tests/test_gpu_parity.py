@@ -343,6 +343,35 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, monkeypat
         _release(dev, ids)
 
 
+@pytest.mark.parametrize("env", [{"LSM_NN_FB": "64"}, {"LSM_NN_FB": "16"},
+                                 {"LSM_NN_FB_FAR": "0.75"}, {"LSM_NN_CERT_FROM": "1"},
+                                 {"LSM_NN_CERT_FROM": "4"}])
+def test_search_path_variants_bit_identical(dev, env, monkeypatch):
+    """The exact 1-NN may be reached along different paths: fallback groups of 16 / 32 / 64
+    lanes, the near/far fallback split, the stability check from pass 1, 2 or 4. Every choice
+    must give the same correspondences, so every result is bit-identical to the default's
+    (C4-style revisit pairs: large initial errors, many fallback queries)."""
+    ps = synthetic.make_revisit_pairs(6, seed=41, model=synthetic.HDL64)
+    ids = _prep(dev, ps.targets + ps.sources, want_normals=True)
+    try:
+        prm = _lib.icp_params(method="p2plane")
+        ref = dev.icp_batch(ids[6:], ids[:6], ps.init, prm)
+        c_ref = dev.last_correspondences()
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        got = dev.icp_batch(ids[6:], ids[:6], ps.init, prm)
+        c_got = dev.last_correspondences()
+        for k in env:
+            monkeypatch.delenv(k)
+        for a, b in zip(ref, got):
+            assert np.array_equal(a["transformation"], b["transformation"])
+            assert a["fitness"] == b["fitness"] and a["inlier_rmse"] == b["inlier_rmse"]
+            assert a["iterations"] == b["iterations"]
+        assert np.array_equal(c_ref, c_got)
+    finally:
+        _release(dev, ids)
+
+
 # ------------------------------------------------------------------ multi-scale chain (C5)
 @pytest.mark.parametrize("method", ["p2plane", "p2p"])
 def test_multiscale_ouster_pair(dev, method):
