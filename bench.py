@@ -11,8 +11,8 @@ Weak scaling: every GPU owns P pairs of one long sequence (distributed.py).
     python bench.py [--gpus N --steps K --warmup W --pairs-per-gpu P]
 
 Prints one JSON line (rank 0) with the roofline of the NN correspondence kernel (HIP events on
-the library's own stream, SURVEY.md §8d algorithmic bytes) and a CPU baseline (the f64 oracle,
-rank 0 at N = 1 only, bounded sample).
+the library's own stream, SURVEY.md §8d algorithmic bytes) and a CPU baseline (the C++/OpenMP f64
+implementation under oracle/cpu, rank 0 at N = 1 only, bounded sample, all threads and 1 thread).
 """
 from __future__ import annotations
 
@@ -52,8 +52,9 @@ def parse():
                     help="hdl64_seq: independent contexts (HIP streams) per GPU, each registering a "
                          "contiguous run of the pairs from its own host thread, so one run's "
                          "latency-bound ICP passes overlap another's normal estimation")
-    ap.add_argument("--cpu-sample-pairs", type=int, default=6,
-                    help="bounded CPU-oracle sample (~10 s on 16 cores for hdl64_seq)")
+    ap.add_argument("--cpu-sample-pairs", type=int, default=24,
+                    help="bounded CPU-baseline sample (~10 s on 16 cores for hdl64_seq; 1/12 of "
+                         "it again on 1 core)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
@@ -78,59 +79,82 @@ def load_or_make_sequence(path, P, seed, model, first, procs):
     return seq
 
 
-def cpu_baseline(seq, n_pairs: int, method: str, threads: int):
-    """The f64 oracle (oracle/open3d_restated.py) on the first n_pairs pairs of the same data."""
-    from oracle import open3d_restated as O
+def _cpu_host():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model or "unknown CPU", os.cpu_count()
+
+
+def _cpu_timed(run, n_pairs: int, threads: int, what: str):
+    """Time run(n) on `threads` OpenMP threads and a smaller sample on 1 thread."""
+    from oracle import cpu_ref as C
     threads = max(1, min(threads, os.cpu_count() or 1))
-    O.WORKERS = threads
+    C.load()
+    C.set_threads(threads)
     t0 = time.perf_counter()
-    pre = []
-    for k in range(n_pairs + 1):
-        pts = O.filter_radius_height(seq.scans[k])
-        nrm = O.estimate_normals(pts) if method == "p2plane" else None
-        pre.append((pts, nrm))
-    for k in range(n_pairs):
-        O.registration_icp(pre[k + 1][0], pre[k][0], 10.0, seq.priors[k], method, pre[k][1])
+    run(n_pairs)
     dt = time.perf_counter() - t0
-    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{n_pairs} consecutive pairs (+{n_pairs + 1} keyframe pre-processes) of "
-                      f"the same synthetic HDL-64 sequence, f64 NumPy/SciPy cKDTree oracle, "
-                      f"{dt:.1f} s"}
+    n1 = max(1, n_pairs // 12)
+    C.set_threads(1)
+    t0 = time.perf_counter()
+    run(n1)
+    dt1 = time.perf_counter() - t0
+    model, ncpu = _cpu_host()
+    return {"value": round(n_pairs / dt, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "value_1core": round(n1 / dt1, 3),
+            "sample": f"{what}: {n_pairs} pairs on {threads} threads ({dt:.1f} s) and {n1} on 1 "
+                      f"thread ({dt1:.1f} s); the C++/OpenMP f64 KD-tree implementation of the "
+                      f"path (oracle/cpu/lsm_cpu.cpp, SURVEY.md 8d) on {model}, nproc {ncpu}"}
+
+
+def cpu_baseline(seq, n_pairs: int, method: str, threads: int):
+    """The CPU implementation on the first pairs of the same sequence (P+1 keyframes pre-processed
+    per P pairs, as in a GPU step)."""
+    from oracle import cpu_ref as C
+
+    def run(n):
+        pre = []
+        for k in range(n + 1):
+            pts = C.filter_radius_height(seq.scans[k])
+            pre.append((pts, C.estimate_normals(pts) if method == "p2plane" else None))
+        for k in range(n):
+            C.registration_icp(pre[k + 1][0], pre[k][0], 10.0, seq.priors[k], method, pre[k][1])
+    return _cpu_timed(run, n_pairs, threads, "consecutive pairs of the same synthetic HDL-64 "
+                                             "sequence")
 
 
 def cpu_baseline_multiscale(seq, n_pairs: int, method: str, threads: int):
-    """The f64 oracle's multi-scale chain on the first n_pairs pairs of the same data."""
-    from oracle import open3d_restated as O
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    O.WORKERS = threads
-    t0 = time.perf_counter()
-    for k in range(n_pairs):
-        O.registration_multiscale(seq.scans[k + 1], seq.scans[k], seq.priors[k], method=method)
-    dt = time.perf_counter() - t0
-    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{n_pairs} pair(s) of the same Ouster-128 sequence through the 3-scale "
-                      f"chain (both keyframes pre-processed per pair), f64 NumPy/SciPy oracle, "
-                      f"{dt:.1f} s"}
+    """The CPU implementation's multi-scale chain on the first pairs of the same data."""
+    from oracle import cpu_ref as C
+
+    def run(n):
+        for k in range(n):
+            C.registration_multiscale(seq.scans[k + 1], seq.scans[k], seq.priors[k], method=method)
+    return _cpu_timed(run, n_pairs, threads, "pairs of the same Ouster-128 sequence through the "
+                                             "3-scale chain (both keyframes pre-processed per pair)")
 
 
 def cpu_baseline_pairs(seq, P: int, n_pairs: int, method: str, threads: int):
-    """The f64 oracle on the first n_pairs independent revisit pairs (both clouds pre-processed)."""
-    from oracle import open3d_restated as O
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    O.WORKERS = threads
-    t0 = time.perf_counter()
-    for k in range(n_pairs):
-        tgt = O.filter_radius_height(seq.scans[k])
-        src = O.filter_radius_height(seq.scans[P + k])
-        nrm = O.estimate_normals(tgt) if method == "p2plane" else None
-        O.filter_radius_height(seq.scans[P + k])
-        if method == "p2plane":
-            O.estimate_normals(src)      # the reference pre-processes both keyframes
-        O.registration_icp(src, tgt, 10.0, seq.priors[k], method, nrm)
-    dt = time.perf_counter() - t0
-    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{n_pairs} revisit pairs (both keyframes pre-processed per pair), f64 "
-                      f"NumPy/SciPy cKDTree oracle, {dt:.1f} s"}
+    """The CPU implementation on the first independent revisit pairs (both clouds pre-processed)."""
+    from oracle import cpu_ref as C
+
+    def run(n):
+        for k in range(n):
+            tgt = C.filter_radius_height(seq.scans[k])
+            src = C.filter_radius_height(seq.scans[P + k])
+            nrm = C.estimate_normals(tgt) if method == "p2plane" else None
+            if method == "p2plane":
+                C.estimate_normals(src)      # the reference pre-processes both keyframes
+            C.registration_icp(src, tgt, 10.0, seq.priors[k], method, nrm)
+    return _cpu_timed(run, n_pairs, threads, "revisit pairs (both keyframes pre-processed per "
+                                             "pair)")
 
 
 def main():

@@ -4,6 +4,10 @@ Only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``b
 import this package, and only as the checker / the timed CPU baseline. The product path
 (``lidar_slam_arvc_amd``) never imports it and never falls back to it.
 
+Two restatements: ``open3d_restated`` (NumPy/SciPy, the reference checker of the tests) and
+``cpu_ref`` (ctypes over ``cpu/lsm_cpu.cpp``, C++/OpenMP f64 with an exact KD-tree: SURVEY.md
+§8d's CPU baseline, timed by bench.py; tests/test_cpu_baseline.py checks it against the former).
+
 Pinning status:
 * filter, loop-closure candidate search, SE(3) host math: pinned bit-exactly against golden
   vectors captured by importing the reference modules in the build container
