@@ -52,9 +52,10 @@ def parse():
                     help="hdl64_seq: independent contexts (HIP streams) per GPU, each registering a "
                          "contiguous run of the pairs from its own host thread, so one run's "
                          "latency-bound ICP passes overlap another's normal estimation")
-    ap.add_argument("--cpu-sample-pairs", type=int, default=24,
-                    help="bounded CPU-baseline sample (~10 s on 16 cores for hdl64_seq; 1/12 of "
-                         "it again on 1 core)")
+    ap.add_argument("--cpu-sample-pairs", type=int, default=0,
+                    help="bounded CPU-baseline sample, 1/12 of it again on 1 core (0: 144 pairs "
+                         "for hdl64_seq, 72 for loop_closure, 16 for ouster_multiscale: ~10 s "
+                         "each on 16 cores of the GPU box's EPYC)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
@@ -318,14 +319,14 @@ def main():
                                            for k in ("nn", "nn_fallback")}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            ns = args.cpu_sample_pairs or (16 if ouster else (72 if loop else 144))
+            ns = max(1, min(ns, P))
             if ouster:
-                cpu = cpu_baseline_multiscale(seq, max(1, args.cpu_sample_pairs // 2),
-                                              args.method, args.cpu_threads)
+                cpu = cpu_baseline_multiscale(seq, ns, args.method, args.cpu_threads)
             elif loop:
-                cpu = cpu_baseline_pairs(seq, P, args.cpu_sample_pairs, args.method,
-                                         args.cpu_threads)
+                cpu = cpu_baseline_pairs(seq, P, ns, args.method, args.cpu_threads)
             else:
-                cpu = cpu_baseline(seq, args.cpu_sample_pairs, args.method, args.cpu_threads)
+                cpu = cpu_baseline(seq, ns, args.method, args.cpu_threads)
         ms_step = dt / args.steps * 1e3
         out = {
             "metric": ("ICP keyframe-pair registrations/sec (256k-ray Ouster-128, multi-scale)"
