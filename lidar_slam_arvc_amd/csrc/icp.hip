@@ -271,16 +271,21 @@ __device__ __forceinline__ float slab_cells2(float f, int k) {
 struct TaskPlan {
     const int32_t *plan;   // [0] active blocks, [1] per-lane blocks
     const int32_t *pref;   // [npairs + 1] prefix of the active pairs' block counts
+    const int32_t *coarse; // [c] the pair holding active block c * PLAN_COARSE
     int npairs;
     int32_t *err;          // set by a one-task-per-workgroup kernel launched on too small a grid
 };
 
 constexpr int PLAN_THREADS = 1024;
+// block -> pair lookup: the pair of every PLAN_COARSE-th block is tabled, the rest is a short
+// forward walk over the prefix (replaces an 11-step binary search over 2000 pairs, a chain of
+// dependent loads at the start of every workgroup of the per-pass kernels)
+constexpr int PLAN_COARSE = 64;
 
 __global__ void __launch_bounds__(PLAN_THREADS)
 plan_kernel(const PairState *__restrict__ st, int npairs, int32_t *__restrict__ pref,
-            int32_t *__restrict__ plan, const uint32_t *__restrict__ active = nullptr,
-            int32_t *poll = nullptr) {
+            int32_t *__restrict__ coarse, int32_t *__restrict__ plan,
+            const uint32_t *__restrict__ active = nullptr, int32_t *poll = nullptr) {
     __shared__ int32_t wsum[PLAN_THREADS / LSM_WAVE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int32_t carry = 0;
@@ -300,7 +305,13 @@ plan_kernel(const PairState *__restrict__ st, int npairs, int32_t *__restrict__ 
             before += q < w ? wsum[q] : 0;
             tot += wsum[q];
         }
-        if (k < npairs) pref[k + 1] = before + x;
+        if (k < npairs) {
+            pref[k + 1] = before + x;
+            // coarse entries c with pref[k] <= c * PLAN_COARSE < pref[k + 1]
+            for (int32_t c = (before + x - v + PLAN_COARSE - 1) / PLAN_COARSE;
+                 c * PLAN_COARSE < before + x; ++c)
+                coarse[c] = k;
+        }
         carry += tot;
         __syncthreads();
     }
@@ -324,13 +335,15 @@ __device__ __forceinline__ int plan_task(const TaskPlan &tp, const PairState *st
     if (m >= per) return -1;
     const int32_t g = l * per + m;
     if (g >= total) return 0;
-    int lo = 0, hi = tp.npairs;   // last pair with pref <= g (it has at least one block)
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (lsm_ld(tp.pref, mid) <= g) lo = mid;
-        else hi = mid;
+    // the pair lo with pref[lo] <= g < pref[lo + 1] (it has at least one block)
+    int lo = lsm_ld(tp.coarse, g / PLAN_COARSE);
+    int32_t p0 = lsm_ld(tp.pref, lo), p1 = lsm_ld(tp.pref, lo + 1);
+    while (p1 <= g) {
+        ++lo;
+        p0 = p1;
+        p1 = lsm_ld(tp.pref, lo + 1);
     }
-    const int32_t blk = g - lsm_ld(tp.pref, lo);
+    const int32_t blk = g - p0;
     task.pair = lo;
     task.start = blk * NN_THREADS;
     task.slot = st[lo].blk0 + blk;
@@ -1263,11 +1276,14 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     double *d_bytes = (double *)ctx->buf("i_bytes", size_t(ncnt) * 8);
     unsigned long long *d_srcn = (unsigned long long *)ctx->buf("i_srcn", size_t(ncnt) * 8);
     int32_t *d_pref = (int32_t *)ctx->buf("i_pref", size_t(npairs + 1) * 4);
+    int64_t nblk_all = 0;
+    for (int64_t k = 0; k < npairs; ++k) nblk_all += ps[k].nblk;
+    int32_t *d_coarse = (int32_t *)ctx->buf("i_coarse", size_t(nblk_all / PLAN_COARSE + 2) * 4);
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
     int32_t *d_err = (int32_t *)ctx->buf("i_err", 4);
     if (!d_corr || !d_cert || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
-        !d_plan || !d_flags || !d_err) {
+        !d_plan || !d_flags || !d_err || !d_coarse) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
     }
@@ -1361,8 +1377,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         if (!d_nst) return LSM_ENOMEM;
         LSM_HIP_TRY(ctx, hipMemsetAsync(d_nst, 0, size_t(ncnt) * (NN_NSTAT + 8) * 8, st));
     }
-    plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
-    const TaskPlan tp{d_plan, d_pref, int(npairs), d_err};
+    plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_coarse, d_plan);
+    const TaskPlan tp{d_plan, d_pref, d_coarse, int(npairs), d_err};
     int64_t queries = 0, queries0 = 0;   // source points searched (timing mode only)
     for (int pass = 0; pass <= max_iter; ++pass) {
         // newest active-pair counts that have landed; waits only to keep at most PASS_LAG
@@ -1435,10 +1451,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                                                        d_srcn + pass, d_flags);
         ctx->toc("solve", ev);
         if (d_poll) {
-            plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan,
+            plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_coarse, d_plan,
                                                     d_active + pass, d_poll + 3 * pass);
         } else {
-            plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_plan);
+            plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_coarse, d_plan);
             LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass, d_active + pass, 4,
                                             hipMemcpyDeviceToHost, st));
             LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass + 1, d_plan, 4,
