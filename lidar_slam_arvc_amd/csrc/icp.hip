@@ -271,7 +271,8 @@ __device__ __forceinline__ float slab_cells2(float f, int k) {
 struct TaskPlan {
     const int32_t *plan;   // [0] active blocks, [1] per-lane blocks
     const int32_t *pref;   // [npairs + 1] prefix of the active pairs' block counts
-    const int32_t *coarse; // [c] the pair holding active block c * PLAN_COARSE
+    const int4 *coarse;    // [c] (pair, pref[pair], pref[pair + 1], blk0) of the pair holding
+                           // active block c * PLAN_COARSE
     int npairs;
     int32_t *err;          // set by a one-task-per-workgroup kernel launched on too small a grid
 };
@@ -284,7 +285,7 @@ constexpr int PLAN_COARSE = 64;
 
 __global__ void __launch_bounds__(PLAN_THREADS)
 plan_kernel(const PairState *__restrict__ st, int npairs, int32_t *__restrict__ pref,
-            int32_t *__restrict__ coarse, int32_t *__restrict__ plan,
+            int4 *__restrict__ coarse, int32_t *__restrict__ plan,
             const uint32_t *__restrict__ active = nullptr, int32_t *poll = nullptr) {
     __shared__ int32_t wsum[PLAN_THREADS / LSM_WAVE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -310,7 +311,7 @@ plan_kernel(const PairState *__restrict__ st, int npairs, int32_t *__restrict__ 
             // coarse entries c with pref[k] <= c * PLAN_COARSE < pref[k + 1]
             for (int32_t c = (before + x - v + PLAN_COARSE - 1) / PLAN_COARSE;
                  c * PLAN_COARSE < before + x; ++c)
-                coarse[c] = k;
+                coarse[c] = make_int4(k, before + x - v, before + x, st[k].blk0);
         }
         carry += tot;
         __syncthreads();
@@ -335,18 +336,23 @@ __device__ __forceinline__ int plan_task(const TaskPlan &tp, const PairState *st
     if (m >= per) return -1;
     const int32_t g = l * per + m;
     if (g >= total) return 0;
-    // the pair lo with pref[lo] <= g < pref[lo + 1] (it has at least one block)
-    int lo = lsm_ld(tp.coarse, g / PLAN_COARSE);
-    int32_t p0 = lsm_ld(tp.pref, lo), p1 = lsm_ld(tp.pref, lo + 1);
-    while (p1 <= g) {
-        ++lo;
-        p0 = p1;
-        p1 = lsm_ld(tp.pref, lo + 1);
+    // the pair lo with pref[lo] <= g < pref[lo + 1] (it has at least one block): usually the
+    // tabled pair itself, else a few steps further
+    const int4 c = lsm_ld(tp.coarse, g / PLAN_COARSE);
+    int lo = c.x;
+    int32_t p0 = c.y, p1 = c.z, b0 = c.w;
+    if (p1 <= g) {
+        do {
+            ++lo;
+            p0 = p1;
+            p1 = lsm_ld(tp.pref, lo + 1);
+        } while (p1 <= g);
+        b0 = st[lo].blk0;
     }
     const int32_t blk = g - p0;
     task.pair = lo;
     task.start = blk * NN_THREADS;
-    task.slot = st[lo].blk0 + blk;
+    task.slot = b0 + blk;
     task.pad = 0;
     return 1;
 }
@@ -1278,7 +1284,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int32_t *d_pref = (int32_t *)ctx->buf("i_pref", size_t(npairs + 1) * 4);
     int64_t nblk_all = 0;
     for (int64_t k = 0; k < npairs; ++k) nblk_all += ps[k].nblk;
-    int32_t *d_coarse = (int32_t *)ctx->buf("i_coarse", size_t(nblk_all / PLAN_COARSE + 2) * 4);
+    int4 *d_coarse = (int4 *)ctx->buf("i_coarse", size_t(nblk_all / PLAN_COARSE + 2) * 16);
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
     int32_t *d_err = (int32_t *)ctx->buf("i_err", 4);
