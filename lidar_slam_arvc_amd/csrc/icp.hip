@@ -51,13 +51,16 @@ struct NNParams {
 
 // Correspondence state of one source point, carried from pass to pass (SoA arrays):
 //   corr[i]  nearest target point (sorted index), -1 = none within max_corr
+//   alt[i]   the search's second-nearest point (sorted index), or -1
 //   cert[i]  (q_s, rho): the f32 query point of the search that found corr[i], and a lower
-//            bound rho on the distance from q_s to every target point OTHER than corr[i] (to
-//            every point when corr[i] = -1), metres.
-// Stability certificate: if the query now sits at q with D = |q - q_s| and |q - t_corr| + D <
-// rho, no other point can be nearer than t_corr, so the nearest neighbour is unchanged and needs
-// no search (and nothing is written). Later ICP passes move the source by micrometres to
-// millimetres, so nearly every query of a converging pair is certified with three loads.
+//            bound rho on the distance from q_s to every target point other than corr[i] and
+//            alt[i] (to every point when corr[i] = -1), metres.
+// Stability certificate: if the query now sits at q with D = |q - q_s|, the nearer w of corr[i]
+// and alt[i] (exact f32 (d2, index) order) is the nearest neighbour whenever |q - w| + D < rho:
+// every other point is at least rho - D away. The pair only swaps places when alt[i] wins. Later
+// ICP passes move the source by micrometres to millimetres, so nearly every query of a
+// converging pair is certified with a few loads; the second point keeps queries whose nearest
+// neighbour flips between two close target points certified.
 struct FallbackItem {
     int32_t pair;
     int32_t i;        // source point (sorted order)
@@ -79,9 +82,9 @@ __device__ __forceinline__ void transform_point(const double *T, float4 p, doubl
     z = T[8] * px + T[9] * py + T[10] * pz + T[11];
 }
 
-// Running (nearest, second-nearest) over examined target points. A point is examined at most
-// once as the current best (k == bidx is skipped: the warm-start point is revisited by the box
-// scan), so the second distance always belongs to a different point.
+// Running (nearest, second-nearest) over examined target points (the fallback's search state).
+// A point is examined at most once as the current best (k == bidx is skipped: the warm-start
+// point is revisited by the box scan), so the second distance always belongs to a different point.
 // `lim` caches prune2(): the squared pruning radius, refreshed whenever bd2 or sd2 changes.
 struct Top2 {
     float bd2;
@@ -116,6 +119,42 @@ __device__ __forceinline__ void top2_add(float d2, int k, Top2 &b) {
         b.sd2 = d2;
     }
     b.lim = prune2(b.bd2, b.sd2, b.m);
+}
+
+// The box search's state: nearest and second-nearest points (both with indices, in (d2, index)
+// order) and the third-smallest distance examined. Pruning at the third distance (capped at
+// (best + m)^2, as prune2) makes the search's rho a bound on every point other than the two, so
+// the certificate can follow the nearest neighbour when it flips to the second point.
+struct Top3 {
+    float bd2;
+    int bidx;
+    float sd2;
+    int sidx;
+    float td2;
+    float lim;   // prune2(bd2, td2, m)
+    float m;
+};
+
+__device__ __forceinline__ Top3 top3_init(int bidx, float bd2, float m) {
+    return Top3{bd2, bidx, INFINITY, -1, INFINITY, prune2(bd2, INFINITY, m), m};
+}
+
+__device__ __forceinline__ void top_add(float d2, int k, Top3 &b) {
+    if (k == b.bidx || k == b.sidx || !(d2 <= b.td2)) return;
+    if (better(d2, k, b.bd2, b.bidx)) {
+        b.td2 = b.sd2;
+        b.sd2 = b.bd2;
+        b.sidx = b.bidx;
+        b.bd2 = d2;
+        b.bidx = k;
+    } else if (better(d2, k, b.sd2, b.sidx)) {
+        b.td2 = b.sd2;
+        b.sd2 = d2;
+        b.sidx = k;
+    } else {
+        b.td2 = d2;
+    }
+    b.lim = prune2(b.bd2, b.td2, b.m);
 }
 
 // The f32 squared distance that ranks candidates: ONE fixed rounding sequence (explicit fmas,
@@ -157,7 +196,7 @@ constexpr int NN_G = LSM_NN_G;
 #endif
 
 __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float qx,
-                                         float qy, float qz, float dyz2, Top2 &t2, uint32_t lin,
+                                         float qy, float qz, float dyz2, Top3 &t2, uint32_t lin,
                                          NNStat *ns = nullptr) {
     NN_ST(ns, 2, 1);
     if (b - a <= lin) {
@@ -168,7 +207,7 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
             for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, min(k + uint32_t(g), b - 1));
 #pragma unroll
             for (int g = 0; g < NN_G; ++g)
-                if (k + uint32_t(g) < b) top2_add(sqd(t[g], qx, qy, qz), int(k + uint32_t(g)), t2);
+                if (k + uint32_t(g) < b) top_add(sqd(t[g], qx, qy, qz), int(k + uint32_t(g)), t2);
         }
         return;
     }
@@ -212,7 +251,7 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
                     stop = true;
                 } else {
                     NN_ST(ns, 4, 1);
-                    top2_add(sqd(t[g], qx, qy, qz), int(k + uint32_t(g)), t2);
+                    top_add(sqd(t[g], qx, qy, qz), int(k + uint32_t(g)), t2);
                 }
             }
         }
@@ -239,7 +278,7 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
                     stop = true;
                 } else {
                     NN_ST(ns, 4, 1);
-                    top2_add(sqd(t[g], qx, qy, qz), k - g, t2);
+                    top_add(sqd(t[g], qx, qy, qz), k - g, t2);
                 }
             }
         }
@@ -383,24 +422,22 @@ constexpr int NN_KCOLD = 2;   // cold start (no previous neighbour): 5x5x5 cells
 // aligned inside the wave); lanes holding the same point merge their second distances.
 // `lim` becomes a valid pruning bound of the whole group: every point some lane skipped is at
 // least that lane's lim away, every examined non-best point at least the merged second.
-__device__ __forceinline__ void group_top2(Top2 &t, int L) {
+// (The only point two lanes can both hold is the warm start; a duplicate third distance only
+// lowers rho, which stays a valid bound.)
+__device__ __forceinline__ void group_top3(Top3 &t, int L) {
     float lim = t.lim;
     for (int off = L >> 1; off > 0; off >>= 1) {
         const float od = __shfl_xor(t.bd2, off, LSM_WAVE);
         const int oi = __shfl_xor(t.bidx, off, LSM_WAVE);
         const float os = __shfl_xor(t.sd2, off, LSM_WAVE);
+        const int osi = __shfl_xor(t.sidx, off, LSM_WAVE);
+        const float ot = __shfl_xor(t.td2, off, LSM_WAVE);
         lim = fminf(lim, __shfl_xor(lim, off, LSM_WAVE));
-        if (oi == t.bidx) {
-            t.sd2 = fminf(t.sd2, os);
-        } else if (better(od, oi, t.bd2, t.bidx)) {
-            t.sd2 = fminf(os, t.bd2);
-            t.bd2 = od;
-            t.bidx = oi;
-        } else {
-            t.sd2 = fminf(t.sd2, od);
-        }
+        if (oi >= 0) top_add(od, oi, t);
+        if (osi >= 0) top_add(os, osi, t);
+        t.td2 = fminf(t.td2, ot);
     }
-    t.lim = fminf(prune2(t.bd2, t.sd2, t.m), lim);
+    t.lim = fminf(prune2(t.bd2, t.td2, t.m), lim);
 }
 
 // Box search of one query by a group of L lanes (sub = this lane's index in the group): the
@@ -411,20 +448,21 @@ __device__ __forceinline__ void group_top2(Top2 &t, int L) {
 // iterating) is not left to one lane. Every lane of the group returns the same values.
 __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, const CloudDev &G,
                                          int i, int prev, float m, const NNParams &prm,
-                                         int &result, float &rho, Top2 &t2, float4 &qp,
+                                         int &result, int &alt, float &rho, Top3 &t2, float4 &qp,
                                          int sub = 0, int L = 1, NNStat *ns = nullptr) {
     NN_ST(ns, 0, 1);
     double qx64, qy64, qz64;
     transform_point(T, lsm_ld(S.xyz, i), qx64, qy64, qz64);
     const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
     qp = make_float4(qx, qy, qz, 0.f);
-    t2 = top2_init(-1, INFINITY, INFINITY, m);
+    t2 = top3_init(-1, INFINITY, m);
     result = -1;
+    alt = -1;
     rho = INFINITY;
     if (G.n <= 0) return true;
     // warm start: the previous pass's nearest neighbour bounds this pass's search. The search
     // stays exact -- the (d2, index) minimum over all points does not depend on the start.
-    if (prev >= 0 && prev < G.n) t2 = top2_init(prev, sqd(lsm_ld(G.xyz, prev), qx, qy, qz), INFINITY, m);
+    if (prev >= 0 && prev < G.n) t2 = top3_init(prev, sqd(lsm_ld(G.xyz, prev), qx, qy, qz), m);
     const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
                 fz = (qz - G.oz) * G.inv_cell;
     // a query outside the target's box searches around the nearest cell of the box: the
@@ -489,11 +527,12 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
                            cz + K + 1 < G.nz ? float(cz + K + 1) - fz : INFINITY);
     const float bound = fminf(bx, fminf(by, bz)) * G.cell;
     const float bound2 = bound * bound * 0.99999f;
-    if (L > 1) group_top2(t2, L);
+    if (L > 1) group_top3(t2, L);
     if (!(t2.bd2 <= bound2 || bound >= prm.maxc)) NN_ST(ns, 7, sub == 0 ? 1 : 0);
     if (t2.bd2 <= bound2 || bound >= prm.maxc) {
         if (t2.bidx >= 0 && t2.bd2 < prm.maxc2) {
             result = t2.bidx;
+            alt = t2.sidx;
             rho = rho_from(t2.lim, bound);
         } else {
             result = -1;
@@ -506,7 +545,7 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
 
 // wave-aggregated append of the lanes with `pending` to the fallback queue
 __device__ __forceinline__ void push_fallback(bool pending, int pair, int i, float m,
-                                              const Top2 &t2,
+                                              const Top3 &t2,
                                               FallbackItem *__restrict__ queue,
                                               uint32_t *__restrict__ queue_n, uint32_t queue_cap) {
     const uint64_t bm = __ballot(pending);
@@ -523,23 +562,26 @@ __device__ __forceinline__ void push_fallback(bool pending, int pair, int i, flo
 }
 
 // Stability check of one query (passes >= 1). cert[g] = (q_s, rho): the f32 query point of the
-// search that found corr[g] and that search's rho (a lower bound on |q_s - t'| for every target
-// point t' other than corr[g]; for every point when corr[g] = -1). For this pass's query point
-// q, every other point is at least rho - D away, D = |q - q_s| (triangle inequality, f64 of the
-// f32 points, rounded up). Certified: |q - t_corr| (1 + 1e-5) + D < rho, i.e. every other point
-// is strictly farther even after the f32 rounding of the search's squared distances (relative
-// error < 1e-6); nothing is written (cert keeps the search's reference point). D is the direct
-// displacement since the search, not a sum of per-pass steps, so a pair that oscillates keeps
-// its certificates. A query without a neighbour stays without one while rho - D >= max_corr
-// (1 + 1e-5); one whose neighbour left max_corr drops it and is re-based at q. Returns false
-// when the query must be searched; `m` is then its margin for the search's rho.
+// search that found corr[g] (and alt[g], its second point, or -1) and that search's rho (a lower
+// bound on |q_s - t'| for every target point t' other than corr[g] and alt[g]; for every point
+// when corr[g] = -1). For this pass's query point q, every such point is at least rho - D away,
+// D = |q - q_s| (triangle inequality, f64 of the f32 points, rounded up). The winner w of
+// corr[g] and alt[g] in the exact f32 (d2, index) order is certified when |q - w| (1 + 1e-5) + D
+// < rho, i.e. every other point is strictly farther even after the f32 rounding of the search's
+// squared distances (relative error < 1e-6); only a swap (alt[g] won) is written, cert keeps
+// the search's reference point. D is the direct displacement since the search, not a sum of
+// per-pass steps, so a pair that oscillates keeps its certificates. A query without a neighbour
+// stays without one while rho - D >= max_corr (1 + 1e-5); one whose neighbour left max_corr drops
+// it and is re-based at q. Returns false when the query must be searched; `m` is then its margin
+// for the search's rho.
 __device__ __forceinline__ float motion_margin(const PairState &P, const float4 s,
                                                const NNParams &prm);
 
 __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &S,
                                            const CloudDev &G, int i, int64_t g,
                                            const NNParams &prm, int32_t *__restrict__ corr,
-                                           float4 *__restrict__ cert, float &m) {
+                                           int32_t *__restrict__ alt, float4 *__restrict__ cert,
+                                           float &m) {
     const float4 s = lsm_ld(S.xyz, i);
     double x, y, z;
     transform_point(P.T, s, x, y, z);
@@ -551,15 +593,31 @@ __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &
     const int prev = corr[g];
     const double r = double(c.w);
     if (prev >= 0) {
-        const float4 t = lsm_ld(G.xyz, prev);
+        const int sec = alt[g];
+        float4 t = lsm_ld(G.xyz, prev);
+        float dt = sqd(t, qx, qy, qz);
+        bool swap = false;
+        if (sec >= 0) {
+            const float4 u = lsm_ld(G.xyz, sec);
+            const float du = sqd(u, qx, qy, qz);
+            if (better(du, sec, dt, prev)) {
+                swap = true;
+                t = u;
+                dt = du;
+            }
+        }
         const double ex = double(qx) - double(t.x), ey = double(qy) - double(t.y),
                      ez = double(qz) - double(t.z);
         const double e = sqrt(ex * ex + ey * ey + ez * ez);
         if (e * (1.0 + 1e-5) + delta < r) {
-            if (sqd(t, qx, qy, qz) >= prm.maxc2) {
+            if (dt >= prm.maxc2) {
                 // the neighbour left max_corr: no point is within it, none nearer than e
                 corr[g] = -1;
+                alt[g] = -1;
                 cert[g] = make_float4(qx, qy, qz, __double2float_rd(fmin(e * (1.0 - 1e-5), r - delta)));
+            } else if (swap) {
+                corr[g] = sec;
+                alt[g] = prev;
             }
             return true;
         }
@@ -594,9 +652,10 @@ __device__ __forceinline__ void flush_stats(const NNStat &ls, unsigned long long
 template <bool CHECK, bool STATS = false>
 __global__ void __launch_bounds__(NN_THREADS)
 nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
-          NNParams prm, int32_t *__restrict__ corr, float4 *__restrict__ cert,
-          FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n, uint32_t queue_cap,
-          uint32_t *__restrict__ searched, unsigned long long *__restrict__ stats = nullptr) {
+          NNParams prm, int32_t *__restrict__ corr, int32_t *__restrict__ alt,
+          float4 *__restrict__ cert, FallbackItem *__restrict__ queue,
+          uint32_t *__restrict__ queue_n, uint32_t queue_cap, uint32_t *__restrict__ searched,
+          unsigned long long *__restrict__ stats = nullptr) {
     NNStat ls{};
     NNStat *ns = STATS ? &ls : nullptr;
     // one task per workgroup: the host sizes the grid from an earlier pass's plan, which only
@@ -619,7 +678,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         __shared__ float s_m[NN_THREADS];
         __shared__ int32_t s_cnt[NN_THREADS / LSM_WAVE];
         bool need = false;
-        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, cert, m);
+        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, alt, cert, m);
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         const uint64_t bm = __ballot(need);
         if (lane == 0) s_cnt[w] = __popcll(bm);
@@ -649,17 +708,18 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         }
         const int sub = int(threadIdx.x) & (L - 1);
         const int64_t g = P.src_off + i;
-        int result = -1;
+        int result = -1, a2 = -1;
         float r = 0.f;
-        Top2 t2 = top2_init(-1, INFINITY, INFINITY, m);
+        Top3 t2 = top3_init(-1, INFINITY, m);
         bool pending = false;
         float4 qp;
         if (live)
-            pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2, qp, sub, L, ns);
+            pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, sub, L, ns);
         const bool lead = live && sub == 0;
         push_fallback(pending && lead, task.pair, i, m, t2, queue, queue_n, queue_cap);
         if (lead) {
             corr[g] = pending ? -2 : result;
+            alt[g] = pending ? -1 : a2;
             if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
         }
         if (STATS) {
@@ -669,18 +729,19 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         return;
     }
     const int64_t g = P.src_off + i;
-    int result = -1;
+    int result = -1, a2 = -1;
     float r = 0.f;
     // a pass >= 1 searched without the check (LSM_NN_CERT_FROM): the search still leaves rho
     // with the margin of this pass's motion, for the next pass's certificate
     if (live && P.iter > 0) m = motion_margin(P, lsm_ld(S.xyz, i), prm);
-    Top2 t2 = top2_init(-1, INFINITY, INFINITY, m);
+    Top3 t2 = top3_init(-1, INFINITY, m);
     bool pending = false;
     float4 qp;
-    if (live) pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, r, t2, qp, 0, 1, ns);
+    if (live) pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, 0, 1, ns);
     push_fallback(pending, task.pair, i, m, t2, queue, queue_n, queue_cap);
     if (live) {
         corr[g] = pending ? -2 : result;
+        alt[g] = pending ? -1 : a2;
         if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
     }
     if (STATS) flush_stats(ls, stats);
@@ -1274,6 +1335,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     const size_t nsrc_tot = size_t(std::max<int64_t>(src_off, 1));
     int32_t *d_corr = (int32_t *)ctx->buf("i_corr", nsrc_tot * 4);
     float4 *d_cert = (float4 *)ctx->buf("i_cert", nsrc_tot * 16);
+    int32_t *d_alt = (int32_t *)ctx->buf("i_alt", nsrc_tot * 4);
     const uint32_t qcap = uint32_t(nsrc_tot);
     FallbackItem *d_q = (FallbackItem *)ctx->buf("i_queue", size_t(qcap) * sizeof(FallbackItem));
     double *d_part = (double *)ctx->buf("i_part", size_t(std::max(slot, 1)) * LSM_ACC * 8);
@@ -1288,7 +1350,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
     int32_t *d_err = (int32_t *)ctx->buf("i_err", 4);
-    if (!d_corr || !d_cert || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
+    if (!d_corr || !d_alt || !d_cert || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
         !d_plan || !d_flags || !d_err || !d_coarse) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
@@ -1300,7 +1362,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_err, 0, 4, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_bytes, 0, size_t(ncnt) * 8, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_srcn, 0, size_t(ncnt) * 8, st));
-    if (src_off > 0) LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
+    if (src_off > 0) {
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_alt, 0xff, size_t(src_off) * 4, st));
+    }
 
     NNParams prm;
     prm.maxc = float(p.max_correspondence_distance);
@@ -1411,15 +1476,15 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             unsigned long long *sp = d_nst + size_t(pass) * NN_NSTAT;
             if (pass < CERT_FROM || nocert)
                 nn_kernel<false, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
             else
                 nn_kernel<true, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
         } else if (pass < CERT_FROM || nocert)
-            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_cert, d_q,
+            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q,
                                                           d_qn + pass, qcap, d_sqn + pass);
         else
-            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_cert, d_q,
+            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q,
                                                          d_qn + pass, qcap, d_sqn + pass);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
