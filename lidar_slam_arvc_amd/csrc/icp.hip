@@ -98,7 +98,7 @@ struct Top2 {
 // never below the best (ties with the best are always examined, so the (d2, index) minimum is
 // exact). Every point the search skips is at least this far, so it is a valid rho (the radius
 // only shrinks during a search). m = 0 gives a plain nearest-neighbour search (rho = best
-// distance: certifies nothing); m = 4 x (this pass's displacement) + 1 mm leaves room for the
+// distance: certifies nothing); m = (this pass's displacement) + 1 mm leaves room for the
 // next passes' motion.
 __device__ __forceinline__ float prune2(float bd2, float sd2, float m) {
     const float c = __builtin_amdgcn_sqrtf(bd2) + m;
@@ -1386,7 +1386,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         const char *e = getenv(k);
         return e ? atof(e) : d;
     };
-    static const double M0 = envf("LSM_NN_M0", 0.0), MMUL = envf("LSM_NN_MMUL", 4.0),
+    static const double M0 = envf("LSM_NN_M0", 0.0), MMUL = envf("LSM_NN_MMUL", 1.0),
                         MADD = envf("LSM_NN_MADD", 1e-3);
     prm.m0 = float(M0);
     static const uint32_t LIN = uint32_t(envf("LSM_NN_LINEAR", 8));
