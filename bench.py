@@ -98,19 +98,23 @@ def _cpu_timed(run, n_pairs: int, threads: int, what: str):
     from oracle import cpu_ref as C
     threads = max(1, min(threads, os.cpu_count() or 1))
     C.load()
+    def timed(n, min_s):   # the sample again until it has run >= min_s (small workloads)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            run(n)
+            done += n
+            dt = time.perf_counter() - t0
+            if dt >= min_s:
+                return done, dt
+
     C.set_threads(threads)
-    t0 = time.perf_counter()
-    run(n_pairs)
-    dt = time.perf_counter() - t0
-    n1 = max(1, n_pairs // 12)
+    n_all, dt = timed(n_pairs, 5.0)
     C.set_threads(1)
-    t0 = time.perf_counter()
-    run(n1)
-    dt1 = time.perf_counter() - t0
+    n1, dt1 = timed(max(1, n_pairs // 12), 5.0)
     model, ncpu = _cpu_host()
-    return {"value": round(n_pairs / dt, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+    return {"value": round(n_all / dt, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
             "value_1core": round(n1 / dt1, 3),
-            "sample": f"{what}: {n_pairs} pairs on {threads} threads ({dt:.1f} s) and {n1} on 1 "
+            "sample": f"{what}: {n_all} pairs on {threads} threads ({dt:.1f} s) and {n1} on 1 "
                       f"thread ({dt1:.1f} s); the C++/OpenMP f64 KD-tree implementation of the "
                       f"path (oracle/cpu/lsm_cpu.cpp, SURVEY.md 8d) on {model}, nproc {ncpu}"}
 
@@ -319,7 +323,7 @@ def main():
                                            for k in ("nn", "nn_fallback")}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            ns = args.cpu_sample_pairs or (16 if ouster else (72 if loop else 144))
+            ns = args.cpu_sample_pairs or (32 if ouster else (72 if loop else 144))
             ns = max(1, min(ns, P))
             if ouster:
                 cpu = cpu_baseline_multiscale(seq, ns, args.method, args.cpu_threads)
