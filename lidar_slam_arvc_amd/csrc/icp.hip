@@ -964,11 +964,11 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
 // ------------------------------------------------------------------------------------------
 // residual / Jacobian accumulation (deterministic block partials)
 // ------------------------------------------------------------------------------------------
-// Wave sums of 32 per-lane values with 32 shuffles instead of 32 x 6: at each butterfly step the
+// Wave sums of 16 per-lane values with 16 shuffles instead of 16 x 6: at each butterfly step the
 // lane pair (l, l ^ off) splits the values it still carries, each half keeping one half of the
-// indices summed over both lanes. After the steps with off = 32 .. 2 and a final off = 1 sum,
-// lane l holds the full wave sum of index l >> 1. Fixed tree: deterministic.
-__device__ __forceinline__ double wave_transpose_sum32(double (&v)[32], int lane) {
+// indices summed over both lanes. After the steps with off = 32 .. 4 and the final off = 2, 1
+// sums, lane l holds the full wave sum of index l >> 2. Fixed tree: deterministic.
+__device__ __forceinline__ double wave_transpose_sum16(double (&v)[16], int lane) {
 #define LSM_TSTEP(OFF, H)                                                     \
     {                                                                         \
         const bool up = (lane & (OFF)) != 0;                                  \
@@ -978,13 +978,35 @@ __device__ __forceinline__ double wave_transpose_sum32(double (&v)[32], int lane
             v[k] = (up ? v[k + (H)] : v[k]) + recv;                           \
         }                                                                     \
     }
-    LSM_TSTEP(32, 16)
-    LSM_TSTEP(16, 8)
-    LSM_TSTEP(8, 4)
-    LSM_TSTEP(4, 2)
-    LSM_TSTEP(2, 1)
+    LSM_TSTEP(32, 8)
+    LSM_TSTEP(16, 4)
+    LSM_TSTEP(8, 2)
+    LSM_TSTEP(4, 1)
 #undef LSM_TSTEP
-    return v[0] + __shfl_xor(v[0], 1, LSM_WAVE);
+    const double s = v[0] + __shfl_xor(v[0], 2, LSM_WAVE);
+    return s + __shfl_xor(s, 1, LSM_WAVE);
+}
+
+// Accumulator k (LSM_ACC layout) of one correspondence. P2Plane: J^T J (upper triangle, row
+// by row: 0-20), J^T r (21-26), r^2 (27); P2P: source (0-2) and target (3-5) sums, t s^T
+// (6-14); both: squared distance (28), count (29).
+template <int METHOD>
+__device__ __forceinline__ double acc_value(int k, const double (&J)[6], double r,
+                                            const double (&sv)[3], const double (&tv)[3],
+                                            double e2) {
+    if (k == 28) return e2;
+    if (k == 29) return 1.0;
+    if (METHOD == LSM_P2PLANE) {
+        constexpr int JA[21] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 5};
+        constexpr int JB[21] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5};
+        if (k < 21) return J[JA[k]] * J[JB[k]];
+        if (k < 27) return J[k - 21] * r;
+        return k == 27 ? r * r : 0.0;
+    }
+    if (k < 3) return sv[k];
+    if (k < 6) return tv[k - 3];
+    if (k < 15) return tv[(k - 6) / 3] * sv[(k - 6) % 3];
+    return 0.0;
 }
 
 template <int METHOD>
@@ -998,54 +1020,53 @@ __device__ __forceinline__ void accumulate_task(const BlockTask task,
     const CloudDev S = cds[P.src];
     const CloudDev G = cds[P.tgt];
     const int i = task.start + threadIdx.x;
-    double acc[30];
-#pragma unroll
-    for (int k = 0; k < 30; ++k) acc[k] = 0.0;
+    // the correspondence's terms; an invalid lane contributes zeros
+    double J[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, sv[3] = {0.0, 0.0, 0.0}, tv[3] = {0.0, 0.0, 0.0};
+    double r = 0.0, e2 = 0.0;
+    bool valid = false;
     if (i < S.n) {
         const int idx = corr[P.src_off + i];
         if (idx >= 0) {
+            valid = true;
             double x, y, z;
             transform_point(P.T, lsm_ld(S.xyz, i), x, y, z);
             const float4 t = lsm_ld(G.xyz, idx);
             const double tx = t.x, ty = t.y, tz = t.z;
             const double ex = x - tx, ey = y - ty, ez = z - tz;
-            acc[28] = (ex * ex + ey * ey) + ez * ez;
-            acc[29] = 1.0;
+            e2 = (ex * ex + ey * ey) + ez * ez;
             if (METHOD == LSM_P2PLANE) {
                 const float4 nf = lsm_ld(G.nrm, idx);
                 const double nx = nf.x, ny = nf.y, nz = nf.z;
-                const double r = (ex * nx + ey * ny) + ez * nz;
-                const double J[6] = {y * nz - z * ny, z * nx - x * nz, x * ny - y * nx, nx, ny, nz};
-                int k = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a)
-#pragma unroll
-                    for (int b = a; b < 6; ++b) acc[k++] = J[a] * J[b];
-#pragma unroll
-                for (int a = 0; a < 6; ++a) acc[21 + a] = J[a] * r;
-                acc[27] = r * r;
+                r = (ex * nx + ey * ny) + ez * nz;
+                J[0] = y * nz - z * ny;
+                J[1] = z * nx - x * nz;
+                J[2] = x * ny - y * nx;
+                J[3] = nx;
+                J[4] = ny;
+                J[5] = nz;
             } else {
-                acc[0] = x;
-                acc[1] = y;
-                acc[2] = z;
-                acc[3] = tx;
-                acc[4] = ty;
-                acc[5] = tz;
-                const double tv[3] = {tx, ty, tz}, sv[3] = {x, y, z};
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] = tv[a] * sv[b];
+                sv[0] = x;
+                sv[1] = y;
+                sv[2] = z;
+                tv[0] = tx;
+                tv[1] = ty;
+                tv[2] = tz;
             }
         }
     }
+    // two halves of 16 accumulators: a transposed wave sum each (fewer live registers than one
+    // of 32), per-wave sums in LDS, then the fixed-order sum over the waves
     __shared__ double red[NN_THREADS / LSM_WAVE][32];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double v[32];
 #pragma unroll
-    for (int k = 0; k < 32; ++k) v[k] = k < 30 ? acc[k] : 0.0;
-    const double sum = wave_transpose_sum32(v, lane);   // lane l: wave sum of index l >> 1
-    if ((lane & 1) == 0) red[w][lane >> 1] = sum;
+    for (int h = 0; h < 2; ++h) {
+        double v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = valid ? acc_value<METHOD>(16 * h + k, J, r, sv, tv, e2) : 0.0;
+        const double sum = wave_transpose_sum16(v, lane);   // lane l: wave sum of index l >> 2
+        if ((lane & 3) == 0) red[w][16 * h + (lane >> 2)] = sum;
+        __builtin_amdgcn_sched_barrier(0);   // keep the halves apart (register pressure)
+    }
     __syncthreads();
     if (threadIdx.x < 30) {
         double s = 0.0;
