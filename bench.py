@@ -225,8 +225,8 @@ def main():
 
         def step():
             n = dev.preprocess(ids, prep)
-            res = dev.icp_batch(ids[P:], ids[:P], seq.priors, icp)
-            rel = np.stack([r["transformation"] for r in res])
+            res = dev.icp_batch_arrays(ids[P:], ids[:P], seq.priors, icp)
+            rel = res["transformation"]
             if group is not None:   # the sequence-level exchange: gather every pair's result
                 allr = [torch.empty(P, 16, dtype=torch.float64, device=cuda) for _ in range(world)]
                 dist.all_gather(allr, torch.from_numpy(rel.reshape(P, 16)).to(cuda))
@@ -246,8 +246,9 @@ def main():
         def run(k, out):
             d, hs = devs[k], run_ids[k]
             n = d.preprocess(hs, prep)
-            out[k] = (n if k == 0 else n[1:], d.icp_batch(hs[1:], hs[:-1],
-                                                          seq.priors[cut[k]:cut[k + 1]], icp))
+            out[k] = (n if k == 0 else n[1:], d.icp_batch_arrays(hs[1:], hs[:-1],
+                                                                 seq.priors[cut[k]:cut[k + 1]],
+                                                                 icp))
 
         def step():
             out = [None] * S
@@ -260,8 +261,8 @@ def main():
             if any(o is None for o in out):
                 raise RuntimeError("a registration run failed")
             n = np.concatenate([o[0] for o in out])
-            res = [r for o in out for r in o[1]]
-            rel = np.stack([r["transformation"] for r in res])
+            res = {key: np.concatenate([o[1][key] for o in out]) for key in out[0][1]}
+            rel = res["transformation"]
             compose_global_sharded(rel, group=group, device=cuda)
             return n, res
 
@@ -300,7 +301,7 @@ def main():
     stats = {k: kstats(k) for k in KERNELS}
     nn = kstats("nn_pass")   # check + search + fallback of every ICP pass
     n_pts, res = last
-    iters = [r["iterations"] for r in res]
+    iters = [r["iterations"] for r in res] if isinstance(res, list) else list(res["iterations"])
     out = None
     if rank == 0:
         achieved = nn["algo_bytes"] / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0

@@ -187,6 +187,12 @@ int lsm_loop_candidates(lsm_ctx *ctx, const double *positions, int64_t m,
 int lsm_loop_triplet_partners(lsm_ctx *ctx, const double *positions, int64_t m,
                               const int64_t *candidates, int64_t n_candidates, int64_t *partner);
 
+/* Chain composition (artelib/homogeneousmatrix.py:184-205 compute_global_transformations, the
+ * serial product run_scanmatcher.py:214-234 applies to the relative transforms) -------------
+ * Host only (no device, no context): out[0] = identity, out[k + 1] = out[k] * rel[k], row-major
+ * 4 x 4 f64, k = 0 .. n - 1 (out holds n + 1 matrices). */
+int lsm_se3_prefix(const double *rel, int64_t n, double *out);
+
 /* Instrumentation ------------------------------------------------------------------------
  * With timing on, the library brackets every launch of the named kernel with HIP events on its
  * own stream and accumulates the durations. Kernel names: "nn" (correspondence search),

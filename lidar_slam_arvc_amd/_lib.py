@@ -27,6 +27,7 @@ EXPORTED = [
     "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
     "lsm_reset_stats", "lsm_ground_plane", "lsm_plane_samples_get", "lsm_split_plane",
     "lsm_fpfh", "lsm_fpfh_download", "lsm_feature_correspondences", "lsm_ransac_feature",
+    "lsm_se3_prefix",
 ]
 
 
@@ -92,6 +93,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "lsm_ground_plane": (C.c_int, [_P, C.c_int64, C.c_double, C.c_double, C.c_int64,
                                        C.c_uint64, C.c_double, _f64p, _i64p, _i64p]),
         "lsm_plane_samples_get": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, _i32p]),
+        "lsm_se3_prefix": (C.c_int, [_f64p, C.c_int64, _f64p]),
         "lsm_split_plane": (C.c_int, [_P, C.c_int64, _f64p, C.c_double, _i64p, _i64p]),
         "lsm_fpfh": (C.c_int, [_P, C.c_int64, C.c_double, C.c_int32, _f64p, C.c_int64]),
         "lsm_fpfh_download": (C.c_int, [_P, C.c_int64, _f64p, C.c_int64]),
@@ -127,6 +129,18 @@ def plane_samples(seed: int, n: int, num_iterations: int) -> np.ndarray:
                                      _ptr(out, C.c_int32))
     if rc != LSM_OK:
         raise ValueError("plane_samples needs n >= 3")
+    return out
+
+
+def se3_prefix(relative) -> np.ndarray:
+    """Serial products of a chain of 4 x 4 transforms (lsm_se3_prefix): out[0] = I,
+    out[k + 1] = out[k] @ relative[k] -- the global poses of compute_global_transformations
+    (artelib/homogeneousmatrix.py:184-205) relative to the first keyframe."""
+    rel = np.ascontiguousarray(np.asarray(relative, dtype=np.float64).reshape(-1, 16))
+    out = np.empty((len(rel) + 1, 4, 4))
+    rc = lib().lsm_se3_prefix(_ptr(rel, C.c_double), len(rel), _ptr(out, C.c_double))
+    if rc != LSM_OK:
+        raise ValueError("lsm_se3_prefix failed")
     return out
 
 
@@ -285,6 +299,17 @@ class Device:
 
     # -- registration ------------------------------------------------------------------------
     def icp_batch(self, src, tgt, init, params: IcpParams):
+        """registration_icp of every (src[k], tgt[k]) pair: a list of result dicts."""
+        a = self.icp_batch_arrays(src, tgt, init, params)
+        T = a["transformation"]
+        fit, rmse = a["fitness"].tolist(), a["inlier_rmse"].tolist()
+        nc, it, stt = a["n_corr"].tolist(), a["iterations"].tolist(), a["status"].tolist()
+        return [dict(transformation=T[k], fitness=fit[k], inlier_rmse=rmse[k], n_corr=nc[k],
+                     iterations=it[k], status=stt[k]) for k in range(len(T))]
+
+    def icp_batch_arrays(self, src, tgt, init, params: IcpParams):
+        """icp_batch with the results as arrays (transformation n x 4 x 4, fitness, inlier_rmse,
+        n_corr, iterations, status): no per-pair Python objects for large batches."""
         s = np.ascontiguousarray(np.atleast_1d(np.asarray(src, dtype=np.int64)))
         t = np.ascontiguousarray(np.atleast_1d(np.asarray(tgt, dtype=np.int64)))
         if len(s) != len(t):
@@ -299,12 +324,10 @@ class Device:
                                           ip, C.byref(params), res), "registration_icp")
         # one structured view of the result array (a per-field ctypes walk costs ~4 us a pair)
         a = np.frombuffer(res, dtype=np.dtype(IcpResult), count=n)
-        T = a["transformation"].reshape(n, 4, 4).copy()
-        fit, rmse = a["fitness"].tolist(), a["inlier_rmse"].tolist()
-        nc, it, stt = (a["correspondences"].tolist(), a["iterations"].tolist(),
-                       a["status"].tolist())
-        return [dict(transformation=T[k], fitness=fit[k], inlier_rmse=rmse[k], n_corr=nc[k],
-                     iterations=it[k], status=stt[k]) for k in range(n)]
+        return dict(transformation=a["transformation"].reshape(n, 4, 4).copy(),
+                    fitness=a["fitness"].copy(), inlier_rmse=a["inlier_rmse"].copy(),
+                    n_corr=a["correspondences"].copy(), iterations=a["iterations"].copy(),
+                    status=a["status"].copy())
 
     def last_correspondences(self) -> np.ndarray:
         n = C.c_int64()

@@ -25,12 +25,10 @@ def shard_pairs(n_pairs: int, world: int, rank: int) -> tuple[int, int]:
 
 
 def local_prefix(relative: np.ndarray) -> np.ndarray:
-    """G[k] = R_0 R_1 ... R_k for the chunk (k = 0 .. n-1); identity-first convention below."""
-    out = np.empty((len(relative) + 1, 4, 4))
-    out[0] = np.eye(4)
-    for k, R in enumerate(relative):
-        out[k + 1] = out[k] @ R
-    return out
+    """G[k] = R_0 R_1 ... R_k for the chunk (k = 0 .. n-1); identity-first convention below.
+    The serial 4 x 4 products run in the library's host code (a NumPy loop costs ~3 us a pair)."""
+    from . import _lib
+    return _lib.se3_prefix(relative)
 
 
 def compose_global_sharded(relative: np.ndarray, T0=None, group=None, device=None) -> np.ndarray:
