@@ -752,6 +752,19 @@ struct ListAcc {
 
 // KDTreeSearchParamHybrid(radius, max_nn) neighbourhood of point j of cloud C by one lane (H: the
 // lane's HSTRIDE-word LDS row), handed to `acc`.
+// Density prediction: a point whose own cell is crowded almost always has more than max_nn
+// ball neighbours, and then scan 1's neighbourhood would be dropped again.
+__device__ __forceinline__ bool predict_dense(const CloudDev &C, const NormalParams &np, float4 qf) {
+    if (!(np.dense_k > 0.f)) return false;
+    auto cc = [](float v, float o, float inv, int n) {
+        const int c = (int)floorf((v - o) * inv);
+        return c < 0 ? 0 : (c > n - 1 ? n - 1 : c);
+    };
+    const int l = lsm_cell_lin(C.nbx, C.nby, cc(qf.x, C.ox, C.inv_cell, C.nx),
+                               cc(qf.y, C.oy, C.inv_cell, C.ny), cc(qf.z, C.oz, C.inv_cell, C.nz));
+    return float(lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l)) >= np.dense_k * C.cell * C.cell;
+}
+
 template <int G, typename Acc>
 __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                             unsigned long long *stats, uint32_t *H, Acc &acc) {
@@ -763,21 +776,9 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
     bool sat = false;
     int count = 0;
-    // Density prediction: a point whose own cell is crowded almost always has more than max_nn
-    // ball neighbours, and then scan 1's neighbourhood would be dropped again. Such points skip
-    // acc.add in scan 1 (histogram only); a wrong guess costs one plain rescan below, which
-    // visits the ball in scan 1's order (identical sums).
-    bool dense = false;
-    if (np.dense_k > 0.f) {
-        auto cc = [](float v, float o, float inv, int n) {
-            const int c = (int)floorf((v - o) * inv);
-            return c < 0 ? 0 : (c > n - 1 ? n - 1 : c);
-        };
-        const int l = lsm_cell_lin(C.nbx, C.nby, cc(qf.x, C.ox, C.inv_cell, C.nx),
-                                   cc(qf.y, C.oy, C.inv_cell, C.ny), cc(qf.z, C.oz, C.inv_cell, C.nz));
-        dense = float(lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l)) >=
-                np.dense_k * C.cell * C.cell;
-    }
+    // Dense-predicted points skip acc.add in scan 1 (histogram only); a wrong guess costs one
+    // plain rescan below, which visits the ball in scan 1's order (identical sums).
+    const bool dense = predict_dense(C, np, qf);
     // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
     // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
     // f32 d^2 and the scale are within 4.2e-7 relative, t < 128). The rest (the sphere's

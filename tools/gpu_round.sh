@@ -17,4 +17,5 @@ tail -1 "$OUT/bench.log"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline > "$OUT/bench_prof.log" 2>&1 || { echo "rocprof failed"; tail -30 "$OUT/bench_prof.log"; exit 1; }
 tail -1 "$OUT/bench_prof.log"
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+rm -rf "$OUT/prof"   # the traces exceed what gpurun copies back (64 MiB); the summary is kept
 head -12 "$OUT/kernel_stats.csv" | cut -c1-220
