@@ -153,6 +153,16 @@ int lsm_split_plane(lsm_ctx *ctx, lsm_cloud cloud, const double plane[4], double
  * compute_fpfh_feature(cloud, KDTreeSearchParamHybrid(radius, max_nn)) (keyframe.py:226-229):
  * FPFH of a pre-processed cloud with normals, kept on the device; `features` (nullable) receives
  * them, n x 33 f64 in reference order. */
+/* The second voxel_down_sample of preprocess_fpfh with a voxel_size (keyframe.py:202-203):
+ * [O3D] PointCloud::VoxelDownSample of a pre-processed cloud WITH normals -- the same voxel keys
+ * and per-voxel point means as lsm_preprocess's voxel pass, computed from the cloud's
+ * reference-order points (the f64 centroids of a voxelised cloud), and per voxel the sum of the
+ * members' non-NaN normals divided by the member count (AccumulatedPoint::GetAverageNormal, not
+ * re-normalised). *out is a NEW pre-processed cloud (voxel-key order) whose normals are those
+ * averages; lsm_cloud_download returns its f64 centroids. LSM_EINVAL: voxel_size <= 0 / too
+ * small (Open3D's LogError cases); LSM_ESTATE: cloud not pre-processed with normals. */
+int lsm_voxel_down_sample_normals(lsm_ctx *ctx, lsm_cloud cloud, double voxel_size,
+                                  lsm_cloud *out);
 int lsm_fpfh(lsm_ctx *ctx, lsm_cloud cloud, double radius, int32_t max_nn, double *features,
              int64_t cap);
 /* Feature.data of the features lsm_fpfh computed last (o3d.pipelines.registration.Feature, read

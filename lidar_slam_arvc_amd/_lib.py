@@ -27,7 +27,7 @@ EXPORTED = [
     "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
     "lsm_reset_stats", "lsm_ground_plane", "lsm_plane_samples_get", "lsm_split_plane",
     "lsm_fpfh", "lsm_fpfh_download", "lsm_feature_correspondences", "lsm_ransac_feature",
-    "lsm_se3_prefix",
+    "lsm_se3_prefix", "lsm_voxel_down_sample_normals",
 ]
 
 
@@ -95,6 +95,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "lsm_plane_samples_get": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, _i32p]),
         "lsm_se3_prefix": (C.c_int, [_f64p, C.c_int64, _f64p]),
         "lsm_split_plane": (C.c_int, [_P, C.c_int64, _f64p, C.c_double, _i64p, _i64p]),
+        "lsm_voxel_down_sample_normals": (C.c_int, [_P, C.c_int64, C.c_double, _i64p]),
         "lsm_fpfh": (C.c_int, [_P, C.c_int64, C.c_double, C.c_int32, _f64p, C.c_int64]),
         "lsm_fpfh_download": (C.c_int, [_P, C.c_int64, _f64p, C.c_int64]),
         "lsm_feature_correspondences": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int32, C.c_int32,
@@ -220,6 +221,15 @@ class Device:
                                             float(threshold), C.byref(g), C.byref(r)),
                    "lsm_split_plane")
         return g.value, r.value
+
+    def voxel_normals(self, cloud: int, voxel_size: float) -> int:
+        """voxel_down_sample of a pre-processed cloud with normals (points averaged, normals
+        averaged and not re-normalised): a new pre-processed cloud handle with those normals."""
+        out = C.c_int64()
+        self.check(self.lib.lsm_voxel_down_sample_normals(self.handle, int(cloud), float(voxel_size),
+                                                          C.byref(out)),
+                   "voxel_down_sample")
+        return out.value
 
     def fpfh(self, cloud: int, radius=0.3, max_nn=100, download=True):
         """compute_fpfh_feature on the device; returns the n x 33 features (reference order)."""

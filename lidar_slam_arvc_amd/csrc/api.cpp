@@ -335,6 +335,31 @@ int lsm_split_plane(lsm_ctx *ctx, lsm_cloud cloud, const double plane[4], double
     return LSM_OK;
 }
 
+int lsm_voxel_down_sample_normals(lsm_ctx *ctx, lsm_cloud cloud, double voxel_size,
+                                  lsm_cloud *out) {
+    if (!ctx || !out) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!c->processed || !c->has_normals) {
+        ctx->set_error("voxel_down_sample with normals needs a pre-processed cloud with normals");
+        return LSM_ESTATE;
+    }
+    (void)hipSetDevice(ctx->device);
+    Cloud *o = new Cloud();
+    const int rc = lsm_voxel_normals_run(ctx, c, voxel_size, o);
+    if (rc != LSM_OK) {
+        free_cloud(o);
+        return rc;
+    }
+    const int64_t id = ctx->next_id++;
+    ctx->clouds[id] = o;
+    *out = id;
+    return LSM_OK;
+}
+
 int lsm_fpfh(lsm_ctx *ctx, lsm_cloud cloud, double radius, int32_t max_nn, double *features,
              int64_t cap) {
     if (!ctx) return LSM_EINVAL;

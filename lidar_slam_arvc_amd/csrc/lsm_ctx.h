@@ -106,6 +106,7 @@ int lsm_split_plane_run(lsm_ctx *ctx, Cloud *c, const double plane[4], double th
                         Cloud *r);
 void lsm_plane_samples(uint64_t seed, int64_t n, int64_t iters, int32_t *out);
 int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn);
+int lsm_voxel_normals_run(lsm_ctx *ctx, Cloud *c, double v, Cloud *o);
 int lsm_feature_corr_run(lsm_ctx *ctx, Cloud *s, Cloud *t, int mutual, int ransac_n,
                          int32_t *out, int64_t cap, int64_t *n_out);
 int lsm_ransac_run(lsm_ctx *ctx, Cloud *src, Cloud *tgt, const int32_t *corr, int64_t ncorr,

@@ -1819,3 +1819,239 @@ int lsm_feature_corr_run(lsm_ctx *ctx, Cloud *s, Cloud *t, int mutual, int ransa
     if (out) std::memcpy(out, h.data(), size_t(std::min(m, cap)) * 8);
     return LSM_OK;
 }
+
+// ------------------------------------------------------------------------------------------
+// voxel_down_sample of a cloud with normals: the second voxelisation of preprocess_fpfh
+// (keyframe.py:202-203). [O3D] VoxelDownSample on a cloud with normals: the same keys and
+// per-voxel point means as the first pass (voxel_keys / voxel_reduce), and per voxel the sum of
+// the members' non-NaN normals divided by the member count (AccumulatedPoint::GetAverageNormal:
+// not re-normalised). Input points are the cloud's reference-order f64 points (the first pass's
+// centroids for a voxelised cloud).
+// ------------------------------------------------------------------------------------------
+namespace {
+
+__global__ void __launch_bounds__(256)
+vn_ref_kernel(const float4 *xyz, const float4 *nrm, const uint32_t *perm, int n, double *P,
+              double *N) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t r = perm[j];
+    if (P) {
+        const float4 p = xyz[j];
+        P[3 * r] = p.x;
+        P[3 * r + 1] = p.y;
+        P[3 * r + 2] = p.z;
+    }
+    const float4 v = nrm[j];
+    N[3 * r] = v.x;
+    N[3 * r + 1] = v.y;
+    N[3 * r + 2] = v.z;
+}
+
+__global__ void __launch_bounds__(256)
+vn_bbox_kernel(const double *P, int n, double *bb) {
+    __shared__ double red[6][256];
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = threadIdx.x; i < n; i += 256)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fmin(lo[a], P[3 * i + a]);
+            hi[a] = fmax(hi[a], P[3 * i + a]);
+        }
+    for (int a = 0; a < 3; ++a) {
+        red[a][threadIdx.x] = lo[a];
+        red[3 + a][threadIdx.x] = hi[a];
+    }
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s)
+            for (int a = 0; a < 3; ++a) {
+                red[a][threadIdx.x] = fmin(red[a][threadIdx.x], red[a][threadIdx.x + s]);
+                red[3 + a][threadIdx.x] = fmax(red[3 + a][threadIdx.x], red[3 + a][threadIdx.x + s]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) bb[threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void __launch_bounds__(256)
+vn_keys_kernel(const double *P, int n, VoxGeo G, double v, uint64_t *keys, uint32_t *vals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t kx = (int64_t)(int)floor(lsm_ddiv(lsm_dsub(P[3 * i], G.ox), v));
+    const int64_t ky = (int64_t)(int)floor(lsm_ddiv(lsm_dsub(P[3 * i + 1], G.oy), v));
+    const int64_t kz = (int64_t)(int)floor(lsm_ddiv(lsm_dsub(P[3 * i + 2], G.oz), v));
+    keys[i] = uint64_t((kx * G.dy + ky) * G.dz + kz);
+    vals[i] = uint32_t(i);
+}
+
+__global__ void __launch_bounds__(256)
+vn_reduce_kernel(const uint64_t *skeys, const uint32_t *svals, const uint32_t *vid,
+                 const uint32_t *flag, uint32_t n, const double *P, const double *N, VoxGeo G,
+                 double *cent, int32_t *vkeys, float *raw, float4 *avgn) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    const uint64_t key = skeys[i];
+    double s[3] = {0.0, 0.0, 0.0}, t[3] = {0.0, 0.0, 0.0};
+    uint32_t j = i;
+    for (; j < n && skeys[j] == key; ++j) {   // members in index order (stable sort)
+        const uint32_t m = svals[j];
+        for (int a = 0; a < 3; ++a) s[a] = lsm_dadd(s[a], P[3 * m + a]);
+        const double nx = N[3 * m], ny = N[3 * m + 1], nz = N[3 * m + 2];
+        if (!isnan(nx) && !isnan(ny) && !isnan(nz)) {
+            t[0] = lsm_dadd(t[0], nx);
+            t[1] = lsm_dadd(t[1], ny);
+            t[2] = lsm_dadd(t[2], nz);
+        }
+    }
+    const double cnt = double(j - i);
+    const uint32_t o = vid[i];
+    double c[3], a3[3];
+    for (int a = 0; a < 3; ++a) {
+        c[a] = lsm_ddiv(s[a], cnt);
+        a3[a] = lsm_ddiv(t[a], cnt);
+        cent[3 * o + a] = c[a];
+        raw[3 * o + a] = float(c[a]);
+    }
+    vkeys[3 * o] = int32_t(int64_t(key / uint64_t(G.dz * G.dy)));
+    vkeys[3 * o + 1] = int32_t(int64_t((key / uint64_t(G.dz)) % uint64_t(G.dy)));
+    vkeys[3 * o + 2] = int32_t(int64_t(key % uint64_t(G.dz)));
+    avgn[o] = make_float4(float(a3[0]), float(a3[1]), float(a3[2]), 0.f);
+}
+
+// normals of a processed cloud from reference-order values: nrm[j] = src[perm[j]]
+__global__ void __launch_bounds__(256)
+vn_adopt_kernel(const float4 *src, const uint32_t *perm, int n, float4 *nrm) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) nrm[j] = src[perm[j]];
+}
+
+}  // namespace
+
+int lsm_voxel_normals_run(lsm_ctx *ctx, Cloud *c, double v, Cloud *o) {
+    hipStream_t st = ctx->stream;
+    if (!(v > 0.0)) {
+        ctx->set_error("voxel_size <= 0.");
+        return LSM_EINVAL;
+    }
+    const int n = int(c->n);
+    double *P = c->voxelized ? c->d_vox : (double *)ctx->buf("vn_P", size_t(std::max(n, 1)) * 24);
+    double *N = (double *)ctx->buf("vn_N", size_t(std::max(n, 1)) * 24);
+    double *d_bb = (double *)ctx->buf("vn_bb", 48);
+    if (!P || !N || !d_bb) return LSM_ENOMEM;
+    VoxGeo G = {0.0, 0.0, 0.0, 1, 1, 1, 0};
+    uint32_t nvox = 0;
+    double *cent = nullptr;
+    int32_t *vkeys = nullptr;
+    float *raw = nullptr;
+    float4 *avgn = nullptr;
+    if (n > 0) {
+        const int nb = (n + 255) / 256;
+        vn_ref_kernel<<<nb, 256, 0, st>>>(c->d_xyz, c->d_nrm, c->d_perm, n,
+                                          c->voxelized ? nullptr : P, N);
+        vn_bbox_kernel<<<1, 256, 0, st>>>(P, n, d_bb);
+        double bb[6];
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(bb, d_bb, 48, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        // the same geometry as run_voxel (Open3D's min_bound - v/2 origin and its range check)
+        const double half = v * 0.5;
+        double vmin[3], vmax[3];
+        for (int a = 0; a < 3; ++a) {
+            vmin[a] = bb[a] - half;
+            vmax[a] = bb[3 + a] + half;
+        }
+        const double ext = std::max(vmax[0] - vmin[0], std::max(vmax[1] - vmin[1], vmax[2] - vmin[2]));
+        if (v * double(std::numeric_limits<int>::max()) < ext) {
+            ctx->set_error("voxel_size is too small.");
+            return LSM_EINVAL;
+        }
+        int64_t d[3];
+        for (int a = 0; a < 3; ++a) d[a] = (int64_t)std::floor((bb[3 + a] - vmin[a]) / v) + 2;
+        const uint64_t cells = uint64_t(d[0]) * uint64_t(d[1]) * uint64_t(d[2]);
+        if (cells > (uint64_t(1) << 44)) {
+            ctx->set_error("voxel grid too large for the 64-bit key space");
+            return LSM_EINVAL;
+        }
+        G = {vmin[0], vmin[1], vmin[2], d[0], d[1], d[2], 0};
+        uint64_t *k_in = (uint64_t *)ctx->buf("v_kin", size_t(n) * 8);
+        uint64_t *k_out = (uint64_t *)ctx->buf("v_kout", size_t(n) * 8);
+        uint32_t *v_in = (uint32_t *)ctx->buf("v_vin", size_t(n) * 4);
+        uint32_t *v_out = (uint32_t *)ctx->buf("v_vout", size_t(n) * 4);
+        uint32_t *flag = (uint32_t *)ctx->buf("v_flag", size_t(n) * 4 + 4);
+        uint32_t *vid = (uint32_t *)ctx->buf("v_vid", size_t(n) * 4 + 4);
+        cent = (double *)ctx->buf("vn_cent", size_t(n) * 24);
+        vkeys = (int32_t *)ctx->buf("vn_keys", size_t(n) * 12);
+        raw = (float *)ctx->buf("vn_raw", size_t(n) * 12);
+        avgn = (float4 *)ctx->buf("vn_avgn", size_t(n) * 16);
+        if (!k_in || !k_out || !v_in || !v_out || !flag || !vid || !cent || !vkeys || !raw || !avgn) {
+            ctx->set_error("scratch allocation failed (voxel normals)");
+            return LSM_ENOMEM;
+        }
+        vn_keys_kernel<<<nb, 256, 0, st>>>(P, n, G, v, k_in, v_in);
+        size_t tmpb = 0;
+        const int endbit = bits_for(cells);
+        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(nullptr, tmpb, k_in, k_out, v_in, v_out, size_t(n), 0,
+                                                   endbit, st));
+        void *tmp = ctx->buf("sort_tmp", tmpb);
+        if (!tmp) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(tmp, tmpb, k_in, k_out, v_in, v_out, size_t(n), 0,
+                                                   endbit, st));
+        voxel_flags<<<nb, 256, 0, st>>>(k_out, uint32_t(n), flag);
+        LSM_HIP_TRY(ctx, hipMemsetAsync(flag + n, 0, 4, st));
+        tmpb = 0;
+        LSM_HIP_TRY(ctx, rocprim::exclusive_scan(nullptr, tmpb, flag, vid, 0u, size_t(n) + 1,
+                                                 rocprim::plus<uint32_t>(), st));
+        tmp = ctx->buf("scan_tmp", tmpb);
+        if (!tmp) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, rocprim::exclusive_scan(tmp, tmpb, flag, vid, 0u, size_t(n) + 1,
+                                                 rocprim::plus<uint32_t>(), st));
+        vn_reduce_kernel<<<nb, 256, 0, st>>>(k_out, v_out, vid, flag, uint32_t(n), P, N, G, cent,
+                                             vkeys, raw, avgn);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(&nvox, vid + n, 4, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    }
+    // the output: a raw cloud of the f32 centroids carrying the averaged normals, pre-processed
+    // with a keep-all filter (grid only), then given those normals and the f64 centroids / keys
+    const int64_t m = std::max<int64_t>(nvox, 1);
+    if (hipMalloc(&o->d_raw, size_t(m) * 12) != hipSuccess ||
+        hipMalloc(&o->d_prior_ref, size_t(m) * 16) != hipSuccess ||
+        hipMalloc(&o->d_vox, size_t(m) * 24) != hipSuccess ||
+        hipMalloc(&o->d_vkeys, size_t(m) * 12) != hipSuccess) {
+        ctx->set_error("hipMalloc failed (voxel normals)");
+        return LSM_ENOMEM;
+    }
+    o->vox_cap = m;
+    o->n_raw = nvox;
+    o->prior_n = nvox;
+    if (nvox) {
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(o->d_raw, raw, size_t(nvox) * 12, hipMemcpyDeviceToDevice, st));
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(o->d_prior_ref, avgn, size_t(nvox) * 16, hipMemcpyDeviceToDevice, st));
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(o->d_vox, cent, size_t(nvox) * 24, hipMemcpyDeviceToDevice, st));
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(o->d_vkeys, vkeys, size_t(nvox) * 12, hipMemcpyDeviceToDevice, st));
+    }
+    lsm_prep_params kp;
+    lsm_default_prep_params(&kp);
+    kp.min_radius = 0.0;
+    kp.max_radius = 1e15;
+    kp.min_height = -1e15;
+    kp.max_height = 1e15;
+    kp.voxel_size = 0.0;
+    kp.want_normals = 0;
+    kp.grid_cell = 0.0;
+    std::vector<Cloud *> one{o};
+    int rc = lsm_prep_batch(ctx, one, kp, nullptr);
+    if (rc) return rc;
+    if (o->n != int64_t(nvox)) {   // a centroid on the z axis (x = y = 0) fails the r > 0 filter
+        ctx->set_error("voxel_down_sample with normals: a centroid lies on the sensor axis");
+        return LSM_EINVAL;
+    }
+    if ((rc = ensure_cloud_buffers(ctx, o, o->n, true))) return rc;
+    if (nvox)
+        vn_adopt_kernel<<<(int(nvox) + 255) / 256, 256, 0, st>>>(o->d_prior_ref, o->d_perm, int(nvox),
+                                                                 o->d_nrm);
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    LSM_HIP_TRY(ctx, hipGetLastError());
+    o->dev.nrm = o->d_nrm;
+    o->has_normals = true;
+    o->voxelized = true;
+    return LSM_OK;
+}

@@ -23,8 +23,9 @@ reference hits UnboundLocalError, keyframe.py:253-255); ``transform`` returns a 
 copy instead of mutating the device-resident filtered cloud; both RANSACs ('icp2planes' plane,
 'fpfh' feature matching) sample from splitmix64(``ransac_seed``) where Open3D uses its unseeded
 RNG, and ``segment_plane`` returns the two parts with their final normals (r = 0.5 ground / 0.3
-rest) already estimated; 'fpfh' with a voxel_size (the reference voxelises twice,
-keyframe.py:193-203) raises NotImplementedError.
+rest) already estimated. 'fpfh' with a voxel_size voxelises twice like the reference
+(keyframe.py:193-203): the second pass (lsm_voxel_down_sample_normals) yields a new device cloud,
+which becomes ``pointcloud_filtered``.
 """
 from __future__ import annotations
 
@@ -150,6 +151,7 @@ class KeyFrame:
         self._filter = None           # (radii, heights) of the current filtered cloud
         self._prep_key = None         # parameters of the current processed cloud
         self._planes = None           # (ground, rest) device handles of 'icp2planes'
+        self._vn = None               # 'fpfh' + voxel_size: handle of the twice-voxelised cloud
         self.ransac_seed = 0          # RANSAC sampler seed (calculate_plane)
 
     # ------------------------------------------------------------------ raw cloud
@@ -188,6 +190,19 @@ class KeyFrame:
                     self._dev.release(h)
             finally:
                 self._planes = None
+        self._release_vn()
+
+    def _release_vn(self):
+        if self._vn is not None:
+            try:
+                self._dev.release(self._vn)
+            finally:
+                self._vn = None
+
+    def _filtered_handle(self):
+        """Device handle behind pointcloud_filtered (the twice-voxelised cloud after 'fpfh' with
+        a voxel_size, else the keyframe's own cloud)."""
+        return self._vn if self._vn is not None else self._handle
 
     def unload_pointcloud(self):
         self._release_planes()
@@ -226,6 +241,7 @@ class KeyFrame:
         if self._handle is None:
             raise RuntimeError("KeyFrame has no point cloud loaded (call load_pointcloud)")
         key = self._key(radii, heights, voxel, normals)
+        self._release_vn()              # pointcloud_filtered goes back to the keyframe's cloud
         if key != self._prep_key:
             self._dev.preprocess([self._handle], self._params(radii, heights, voxel, normals))
             self._prep_key = key
@@ -262,10 +278,14 @@ class KeyFrame:
 
     # ------------------------------------------------------------------ FPFH (§8f row 4)
     def preprocess_fpfh(self):
-        if self.voxel_size is not None:
-            raise NotImplementedError("'fpfh' with a voxel_size (the reference voxelises twice, "
-                                      "keyframe.py:193-203) is not on the MI355X path")
-        self.preprocess_icp2planes()        # filter, normals, plane, split, part normals
+        self._run(None, None, self.voxel_size, True)         # filter (+ voxel), normals
+        if self.voxel_size is not None:                      # keyframe.py:202-203
+            self._vn = self._dev.voxel_normals(self._handle, self.voxel_size)
+            self.pointcloud_filtered = DevicePointCloud(self._dev, self._vn, True)
+        self.plane_model = self.calculate_plane(pcd=self.pointcloud_filtered)
+        g, ng = self.segment_plane(self.plane_model, pcd=self.pointcloud_filtered)
+        self.pointcloud_ground_plane = g
+        self.pointcloud_non_ground_plane = ng
         self._dev.fpfh(self._planes[1], self.voxel_size_normals, 100, download=False)
         self.pointcloud_fpfh = FeatureHandle(self._dev, self._planes[1], self.voxel_size_normals,
                                              100)
@@ -281,7 +301,7 @@ class KeyFrame:
         r = self._dev.ransac_feature(src, tgt, corres, self.fpfh_threshold, 0.9, 100000, 0.999,
                                      seed=self.ransac_seed)
         self.last_ransac = r
-        res = self._dev.icp_batch([other._handle], [self._handle],
+        res = self._dev.icp_batch([other._filtered_handle()], [self._filtered_handle()],
                                   r["transformation"].reshape(1, 16),
                                   self.registration_params("pointplane"))[0]
         self.last_registration = res
@@ -297,22 +317,26 @@ class KeyFrame:
 
     def calculate_plane(self, pcd=None, height=-0.5, thresholdA=0.01):
         """RANSAC ground plane [a, b, c, d] of the points below `height` (keyframe.py:417-437)."""
-        if pcd is not None and getattr(pcd, "_handle", self._handle) != self._handle:
+        h = self._filtered_handle()
+        if pcd is not None and getattr(pcd, "_handle", h) != h:
             raise ValueError("calculate_plane works on this keyframe's device cloud")
-        if self._handle is None or self._prep_key is None:
+        if h is None or self._prep_key is None:
             raise RuntimeError("calculate_plane needs a pre-processed keyframe")
-        plane, _, _ = self._dev.ground_plane(self._handle, height, thresholdA, 1000,
+        plane, _, _ = self._dev.ground_plane(h, height, thresholdA, 1000,
                                              seed=self.ransac_seed)
         return plane.tolist()
 
     def segment_plane(self, plane_model, pcd=None, thresholdB=0.4):
         """(ground, non-ground) clouds within / beyond thresholdB of the plane
         (keyframe.py:439-461), resident on the device with their normals."""
-        if pcd is not None and getattr(pcd, "_handle", self._handle) != self._handle:
+        h = self._filtered_handle()
+        if pcd is not None and getattr(pcd, "_handle", h) != h:
             raise ValueError("segment_plane works on this keyframe's device cloud")
-        self._release_planes()
-        g, ng = self._dev.split_plane(self._handle, np.asarray(plane_model, dtype=np.float64),
-                                      thresholdB)
+        if self._planes is not None:
+            for p in self._planes:
+                self._dev.release(p)
+            self._planes = None
+        g, ng = self._dev.split_plane(h, np.asarray(plane_model, dtype=np.float64), thresholdB)
         self._planes = (g, ng)
         keep_all = dict(min_radius=0.0, max_radius=1e15, min_height=-1e15, max_height=1e15,
                         max_nn=ICP_PARAMETERS.max_nn_gd, want_normals=True)

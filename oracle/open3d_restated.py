@@ -44,12 +44,15 @@ def filter_radius_height(points, min_radius=MIN_RADIUS, max_radius=MAX_RADIUS,
 INT_MAX = 2147483647
 
 
-def voxel_down_sample(points, voxel_size):
+def voxel_down_sample(points, voxel_size, normals=None):
     """Open3D VoxelDownSample: min_bound - v/2 origin, floor((p - o) / v) keys, per-voxel mean.
 
     Returns (keys K x 3 int64, centroids K x 3 float64) sorted lexicographically by key
     (Open3D's own output order is unordered_map iteration order, i.e. unspecified). Sums run in
     point-index order, as Open3D's AccumulatedPoint does, so centroids are bit-reproducible.
+    With `normals` (a cloud that has normals, keyframe.py:202-203) the result is
+    (keys, centroids, averaged normals): AccumulatedPoint::AddPoint adds a member's normal unless
+    a component is NaN, GetAverageNormal divides by the member count, nothing re-normalises.
     """
     p = np.asarray(points, dtype=np.float64)
     if voxel_size <= 0.0:
@@ -69,12 +72,21 @@ def voxel_down_sample(points, voxel_size):
     ends = np.append(starts[1:], len(ks))
     cent = np.empty((len(starts), 3))
     ps = p[order]
+    ns = None if normals is None else np.asarray(normals, dtype=np.float64)[order]
+    avg = None if normals is None else np.empty((len(starts), 3))
     for v, (a, b) in enumerate(zip(starts, ends)):
         acc = np.zeros(3)
+        nacc = np.zeros(3)
         for i in range(a, b):                 # sequential, index order (AccumulatedPoint::AddPoint)
             acc = acc + ps[i]
+            if ns is not None and not np.isnan(ns[i]).any():
+                nacc = nacc + ns[i]
         cent[v] = acc / float(b - a)
-    return ks[starts], cent
+        if avg is not None:
+            avg[v] = nacc / float(b - a)
+    if normals is None:
+        return ks[starts], cent
+    return ks[starts], cent, avg
 
 
 # --------------------------------------------------------------------------------------------
@@ -821,12 +833,22 @@ def ransac_feature_matching(source, target, corres, max_corr=5.0, edge=0.9, max_
     return best
 
 
-def preprocess_fpfh(points_raw, seed=0):
-    """KeyFrame.preprocess_fpfh (keyframe.py:191-229) for voxel_size None: filter, normals
-    (r 0.3, max_nn 300), ground plane + split, normals of both parts oriented to the first ones
-    (r 0.5 ground, 0.3 rest), FPFH of the non-ground part (r 0.3, max_nn 100)."""
+def preprocess_fpfh(points_raw, seed=0, voxel_size=None, first_normals=None):
+    """KeyFrame.preprocess_fpfh (keyframe.py:191-229): filter (+ voxel, :193-194), normals
+    (r 0.3, max_nn 300), with a voxel_size a second voxel_down_sample of the cloud WITH its
+    normals (:202-203: centroids of centroids, averaged normals), ground plane + split, normals of
+    both parts oriented to the carried ones (r 0.5 ground, 0.3 rest), FPFH of the non-ground part
+    (r 0.3, max_nn 100). `points` / `normals` are pointcloud_filtered's (the P2Plane target of
+    global_registration's refinement). `first_normals` (tests) replaces the first estimate_normals
+    result: unoriented normals carry an arbitrary sign per point, which the second voxelisation's
+    averaging turns into different magnitudes, so a check of the later steps feeds both sides the
+    same first normals."""
     P = filter_radius_height(points_raw)
-    N = estimate_normals(P)
+    if voxel_size is not None:
+        P = voxel_down_sample(P, voxel_size)[1]
+    N = estimate_normals(P) if first_normals is None else np.asarray(first_normals, np.float64)
+    if voxel_size is not None:
+        _, P, N = voxel_down_sample(P, voxel_size, normals=N)
     plane = calculate_plane(P, seed=seed)
     a, b, c, d = plane
     dist = np.abs(a * P[:, 0] + b * P[:, 1] + c * P[:, 2] + d) / np.sqrt(a * a + b * b + c * c)

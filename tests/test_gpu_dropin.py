@@ -77,10 +77,12 @@ def test_keyframe_voxel_and_filters(euroc):
     kf.pre_process("icppointplane")
     assert kf.pointcloud_filtered.has_normals()
     assert np.allclose(np.linalg.norm(kf.pointcloud_filtered.normals, axis=1), 1.0, atol=1e-5)
-    with pytest.raises(NotImplementedError):
-        kf.pre_processed = False
-        kfm.method = "fpfh"
-        kf.pre_process("fpfh")
+    n_once = len(kf.pointcloud_filtered)
+    kf.pre_process("fpfh")                 # voxelised twice (keyframe.py:193-203): a new cloud
+    assert kf._vn is not None and 0 < len(kf.pointcloud_filtered) <= n_once
+    assert kf.pointcloud_filtered.has_normals()
+    kf.pre_process("icppointplane")        # pointcloud_filtered is the keyframe's cloud again
+    assert kf._vn is None and len(kf.pointcloud_filtered) == n_once
     with pytest.raises(ValueError):
         kf.local_registration_simple(kf, None, option="bogus")
 

@@ -72,3 +72,83 @@ def test_ransac_seeded_and_errors(fpfh_pair):
     assert r1["fitness"] == r2["fitness"] and r1["evaluated"] == r2["evaluated"]
     with pytest.raises(RuntimeError, match="out of range"):
         dev.ransac_feature(ks._planes[1], kt._planes[1], np.array([[10**7, 0]] * 4))
+
+
+# ---- 'fpfh' with a voxel_size: the reference voxelises twice (keyframe.py:193-194, :202-203),
+# the second time a cloud that has normals (centroids of centroids, averaged normals)
+VOXEL = 0.2
+
+
+@pytest.fixture(scope="module")
+def fpfh_pair_voxel(tmp_path_factory):
+    seq = synthetic.make_sequence(2, seed=3, model=synthetic.HDL64)
+    d = str(tmp_path_factory.mktemp("fpfh_vox"))
+    times = datasets.write_euroc(d, seq)
+    kfm = KeyFrameManager(d, np.array(times), voxel_size=VOXEL, method="fpfh")
+    for i in range(2):
+        kfm.add_keyframe(i)
+        kfm.load_pointcloud(i)
+        kfm.pre_process(i)
+    # the oracle's later steps from the device's first normals (sign-free equal to the oracle's
+    # own, below): an unoriented normal's sign is arbitrary per point and the second voxelisation
+    # averages normals, so only the same first normals give comparable averages
+    first = [kf._dev.download(kf._handle, normals=True) for kf in kfm.keyframes]
+    ref = [O.preprocess_fpfh(s, voxel_size=VOXEL, first_normals=f[1])
+           for s, f in zip(seq.scans, first)]
+    for s, (p1, n1) in zip(seq.scans, first):
+        own = O.voxel_down_sample(O.filter_radius_height(s), VOXEL)[1]
+        assert np.array_equal(p1, own)
+        dots = np.abs(np.sum(n1 * O.estimate_normals(own), axis=1))
+        assert np.mean(dots > 1 - 1e-5) > 0.999
+    yield seq, kfm, ref
+    for i in range(2):
+        kfm.unload_pointcloud(i)
+
+
+def test_fpfh_voxel_second_pass(fpfh_pair_voxel):
+    seq, kfm, ref = fpfh_pair_voxel
+    for kf, r in zip(kfm.keyframes, ref):
+        pf = kf.pointcloud_filtered
+        # keys from the first pass's f64 centroids, sums in the same member order: bit-exact
+        assert np.array_equal(pf.points, r["points"])
+        # averaged (not re-normalised) normals: the same f64 sums, stored as f32
+        assert np.abs(pf.normals - r["normals"]).max() < 1e-6
+        assert np.all(np.linalg.norm(pf.normals, axis=1) <= 1 + 1e-6)
+        ng = kf.pointcloud_non_ground_plane
+        # the split parts are new device clouds: f32 points, split on the exact f64 distances
+        assert np.array_equal(ng.points, r["rest"].astype(np.float32).astype(np.float64))
+        dots = np.sum(ng.normals * r["rest_normals"], axis=1)
+        assert np.mean(dots > 1 - 1e-5) > 0.99
+        F = kf.pointcloud_fpfh.data.T
+        assert F.shape == r["fpfh"].shape
+        # the FPFH kernel on its own inputs (the f32 part points, the device part normals)
+        own = O.compute_fpfh(ng.points, ng.normals, 0.3, 100)
+        close = np.all(np.abs(F - own) < 1e-6 * (1 + np.abs(own)), axis=1)
+        assert close.mean() > 0.99
+        # against the f64 chain: the parts' f32 rounding moves some pair features across bin edges
+        close = np.all(np.abs(F - r["fpfh"]) < 1e-5 * (1 + np.abs(r["fpfh"])), axis=1)
+        assert close.mean() > 0.95
+
+
+def test_fpfh_voxel_global_registration(fpfh_pair_voxel):
+    seq, kfm, ref = fpfh_pair_voxel
+    T = kfm.compute_transformation(0, 1, se3.HomogeneousMatrix(np.eye(4)))
+    icp, r, _ = O.global_registration(ref[1], ref[0])
+    assert np.abs(T.array[:3, :3] - icp["transformation"][:3, :3]).max() < 1e-4
+    assert np.abs(T.array[:3, 3] - icp["transformation"][:3, 3]).max() < 1e-3
+
+
+def test_voxel_normals_errors(fpfh_pair_voxel):
+    seq, kfm, ref = fpfh_pair_voxel
+    dev = kfm._dev
+    kf = kfm.keyframes[0]
+    with pytest.raises(RuntimeError, match="voxel_size <= 0"):
+        dev.voxel_normals(kf._handle, 0.0)
+    with pytest.raises(RuntimeError, match="too small"):
+        dev.voxel_normals(kf._handle, 1e-12)
+    raw = dev.upload(seq.scans[0])
+    try:
+        with pytest.raises(RuntimeError, match="normals"):
+            dev.voxel_normals(raw, VOXEL)          # not pre-processed with normals
+    finally:
+        dev.release(raw)

@@ -32,6 +32,21 @@ def test_voxel_keys_hand_computed():
         O.voxel_down_sample(np.array([[0, 0, 0], [1e10, 0, 0]]), 1e-3)
 
 
+def test_voxel_normals_averaged_not_renormalised():
+    # preprocess_fpfh's second voxel_down_sample (keyframe.py:202-203) of a cloud with normals:
+    # AccumulatedPoint sums the non-NaN normals and divides by the member count
+    v = 0.5
+    p = np.array([[0.0, 0.0, 0.0], [0.1, 0.0, 0.0], [0.2, 0.0, 0.0], [2.0, 0.0, 0.0]])
+    n = np.array([[0.0, 0.0, 1.0], [1.0, 0.0, 0.0], [np.nan, 0.0, 0.0], [0.0, 1.0, 0.0]])
+    keys, cent, avg = O.voxel_down_sample(p, v, normals=n)
+    assert keys.tolist() == [[0, 0, 0], [4, 0, 0]]
+    assert np.array_equal(cent[0], ((p[0] + p[1]) + p[2]) / 3.0)
+    assert np.array_equal(avg[0], np.array([1.0, 0.0, 1.0]) / 3.0)   # NaN member counted, not added
+    assert np.array_equal(avg[1], [0.0, 1.0, 0.0])
+    k2, c2 = O.voxel_down_sample(p, v)                                 # same points without normals
+    assert np.array_equal(k2, keys) and np.array_equal(c2, cent)
+
+
 def test_fast_eigen_matches_eigh():
     rng = np.random.default_rng(0)
     A = rng.normal(size=(500, 3, 3))
