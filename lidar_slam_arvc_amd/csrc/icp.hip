@@ -48,6 +48,7 @@ struct NNParams {
     uint32_t lin;      // runs of at most this many points are scanned whole (no entry search)
     double m_mul, m_add;   // rho margin of a search after a pass that moved the query by dq
     float direct_rc;   // warm-start distance (cells) from which a query skips the box search
+    int direct_iter;   // ... once its pair has made this many updates
 };
 
 // Correspondence state of one source point, carried from pass to pass (SoA arrays):
@@ -416,9 +417,12 @@ __device__ __forceinline__ int plan_task(const TaskPlan &tp, const PairState *st
 // faces not clipped by the grid), else queued for the fallback.
 constexpr int NN_KMAX = 4;
 constexpr int NN_KCOLD = 2;   // cold start (no previous neighbour): 5x5x5 cells
-// warm starts at least this many cells away skip the box search (nn_query); measured per 1999-pair
-// step (nn + fallback ms): off 99.7, 6 98.7, 5 98.1, 4 96.4, 3 92.1, 2.5 92.3, 2 93.8, 1.5 98.2
+// In pairs with >= NN_DIRECT_ITER updates, warm starts at least NN_DIRECT_RC cells away skip the
+// box search (nn_query). nn + fallback ms per step, C3 (1999 sequence pairs) / C4 (512 revisit
+// pairs): off 100.4 / 64.7; 3 cells from update 0: 92.5 / 93.6; from 4: 92.9 / 71.5; from 12:
+// 93.5 / 66.8; from 20: 94.8 / 66.1; 4 cells from 12: 97.2 / 64.4
 constexpr double NN_DIRECT_RC = 3.0;
+constexpr int NN_DIRECT_ITER = 12;
 
 // Returns true when resolved (result / rho set), false when the fallback must finish it (t2
 // holds what the box search found).
@@ -453,7 +457,8 @@ __device__ __forceinline__ void group_top3(Top3 &t, int L) {
 __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, const CloudDev &G,
                                          int i, int prev, float m, const NNParams &prm,
                                          int &result, int &alt, float &rho, Top3 &t2, float4 &qp,
-                                         int sub = 0, int L = 1, NNStat *ns = nullptr) {
+                                         int sub = 0, int L = 1, NNStat *ns = nullptr,
+                                         bool direct_ok = false) {
     NN_ST(ns, 0, 1);
     double qx64, qy64, qz64;
     transform_point(T, lsm_ld(S.xyz, i), qx64, qy64, qz64);
@@ -477,12 +482,15 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     int K = NN_KCOLD;
     if (t2.bd2 < INFINITY) {
         const float rc = sqrtf(t2.bd2) * G.inv_cell * 1.0001f + 1e-4f;
-        // A previous neighbour this far out (>= NN_DIRECT_RC cells) needs a wide box, which
-        // settles the query only when a point turns up within its face distance; far queries
-        // (no target surface near them, which no certificate carries either) mostly fail it
-        // after walking ~40 rows. They go straight to the fallback with the warm start as their
-        // best, which finds the same (d2, index) minimum with 32 lanes over 1.5 m blocks.
-        if (rc >= prm.direct_rc) {
+        // In a pair that keeps iterating (direct_ok: >= NN_DIRECT_ITER updates, the chaotic
+        // tail), a query whose previous neighbour lies >= NN_DIRECT_RC cells away needs a wide
+        // box, which settles it only when a point turns up within the box's face distance; there
+        // such queries (no target surface near them) mostly fail it after walking ~40 rows. They
+        // go straight to the fallback with the warm start as their best, which finds the same
+        // (d2, index) minimum with 32 lanes over 1.5 m blocks. Early passes keep the box search:
+        // after a large first correction (revisit pairs) the surface is often near again, and
+        // the fallback, starting from the stale warm start, costs more than the box.
+        if (direct_ok && rc >= prm.direct_rc) {
             NN_ST(ns, 7, sub == 0 ? 1 : 0);
             return false;
         }
@@ -727,7 +735,8 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         bool pending = false;
         float4 qp;
         if (live)
-            pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, sub, L, ns);
+            pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, sub, L, ns,
+                                P.iter >= prm.direct_iter);
         const bool lead = live && sub == 0;
         push_fallback(pending && lead, task.pair, i, m, t2, queue, queue_n, queue_cap);
         if (lead) {
@@ -750,7 +759,9 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
     Top3 t2 = top3_init(-1, INFINITY, m);
     bool pending = false;
     float4 qp;
-    if (live) pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, 0, 1, ns);
+    if (live)
+        pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, 0, 1, ns,
+                            P.iter >= prm.direct_iter);
     push_fallback(pending, task.pair, i, m, t2, queue, queue_n, queue_cap);
     if (live) {
         corr[g] = pending ? -2 : result;
@@ -1431,6 +1442,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         // straight to the fallback; <= 0 turns it off
         const double d = envf("LSM_NN_DIRECT", NN_DIRECT_RC);
         prm.direct_rc = d > 0.0 ? float(d) : INFINITY;
+        prm.direct_iter = int(envf("LSM_NN_DIRECT_ITER", NN_DIRECT_ITER));
     }
 
     // Passes are launched back to back; the plan of each pass is rebuilt on the device after the

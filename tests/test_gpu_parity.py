@@ -346,11 +346,13 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, monkeypat
 @pytest.mark.parametrize("env", [{"LSM_NN_FB": "64"}, {"LSM_NN_FB": "16"},
                                  {"LSM_NN_FB_FAR": "0.75"}, {"LSM_NN_CERT_FROM": "1"},
                                  {"LSM_NN_CERT_FROM": "4"}, {"LSM_NN_DIRECT": "0"},
-                                 {"LSM_NN_DIRECT": "1"}, {"LSM_NN_DIRECT": "2.5"}])
+                                 {"LSM_NN_DIRECT": "1", "LSM_NN_DIRECT_ITER": "0"},
+                                 {"LSM_NN_DIRECT": "2.5", "LSM_NN_DIRECT_ITER": "1"}])
 def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     """The exact 1-NN may be reached along different paths: fallback groups of 16 / 32 / 64
     lanes, the near/far fallback split, the stability check from pass 1, 2 or 4, queries with a
-    far warm start sent straight to the fallback from 1 / 2.5 / 3 (default) cells or never. Every choice
+    far warm start sent straight to the fallback (from 1 cell in every pass, from 2.5 cells
+    after the first update, the default 3 cells after 12 updates, or never). Every choice
     must give the same correspondences, so every result is bit-identical to the default's
     (C4-style revisit pairs: large initial errors, many fallback queries)."""
     ps = synthetic.make_revisit_pairs(6, seed=41, model=synthetic.HDL64)
