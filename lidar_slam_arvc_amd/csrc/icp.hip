@@ -783,6 +783,23 @@ __device__ __forceinline__ float gap2(float q, float lo, float hi) {
 __device__ __forceinline__ int ring_size(int r) { return r == 0 ? 1 : 24 * r * r + 2; }
 __device__ __forceinline__ int ring_prefix(int r) { return r == 0 ? 0 : (2 * r - 1) * (2 * r - 1) * (2 * r - 1); }
 constexpr int FB_R0 = 2;   // the fallback's first shell: rings 0 .. FB_R0 (5 x 5 x 5 blocks)
+// the first shell's block offsets (dx, dy, dz) centre-out, by |offset|^2: the blocks nearest the
+// query are scanned first, so the pruning radius shrinks before the outer blocks are tested
+__constant__ int8_t c_shell[3 * 125] = {
+    0, 0, 0, 0, 0, -1, 0, -1, 0, -1, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0, 1, 0, -1, -1, -1, 0, -1, 1, 0, -1,
+    0, 1, -1, -1, -1, 0, 1, -1, 0, -1, 1, 0, 1, 1, 0, 0, -1, 1, -1, 0, 1, 1, 0, 1, 0, 1, 1, -1, -1, -1,
+    1, -1, -1, -1, 1, -1, 1, 1, -1, -1, -1, 1, 1, -1, 1, -1, 1, 1, 1, 1, 1, 0, 0, -2, 0, -2, 0, -2, 0, 0,
+    2, 0, 0, 0, 2, 0, 0, 0, 2, 0, -1, -2, -1, 0, -2, 1, 0, -2, 0, 1, -2, 0, -2, -1, -2, 0, -1, 2, 0, -1,
+    0, 2, -1, -1, -2, 0, 1, -2, 0, -2, -1, 0, 2, -1, 0, -2, 1, 0, 2, 1, 0, -1, 2, 0, 1, 2, 0, 0, -2, 1,
+    -2, 0, 1, 2, 0, 1, 0, 2, 1, 0, -1, 2, -1, 0, 2, 1, 0, 2, 0, 1, 2, -1, -1, -2, 1, -1, -2, -1, 1, -2,
+    1, 1, -2, -1, -2, -1, 1, -2, -1, -2, -1, -1, 2, -1, -1, -2, 1, -1, 2, 1, -1, -1, 2, -1, 1, 2, -1, -1, -2, 1,
+    1, -2, 1, -2, -1, 1, 2, -1, 1, -2, 1, 1, 2, 1, 1, -1, 2, 1, 1, 2, 1, -1, -1, 2, 1, -1, 2, -1, 1, 2,
+    1, 1, 2, 0, -2, -2, -2, 0, -2, 2, 0, -2, 0, 2, -2, -2, -2, 0, 2, -2, 0, -2, 2, 0, 2, 2, 0, 0, -2, 2,
+    -2, 0, 2, 2, 0, 2, 0, 2, 2, -1, -2, -2, 1, -2, -2, -2, -1, -2, 2, -1, -2, -2, 1, -2, 2, 1, -2, -1, 2, -2,
+    1, 2, -2, -2, -2, -1, 2, -2, -1, -2, 2, -1, 2, 2, -1, -2, -2, 1, 2, -2, 1, -2, 2, 1, 2, 2, 1, -1, -2, 2,
+    1, -2, 2, -2, -1, 2, 2, -1, 2, -2, 1, 2, 2, 1, 2, -1, 2, 2, 1, 2, 2, -2, -2, -2, 2, -2, -2, -2, 2, -2,
+    2, 2, -2, -2, -2, 2, 2, -2, 2, -2, 2, 2, 2, 2, 2,
+};
 
 // Chebyshev ring r of blocks around the origin block: t in [0, 24 r^2 + 2) -> offset.
 __device__ __forceinline__ void ring_offset(int r, int t, int &dx, int &dy, int &dz) {
@@ -893,14 +910,13 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                     if (sub == 0) fs[2] += 1;
                     const int t = b0 + sub;
                     uint32_t a = 0, b = 0;
+                    float lb = INFINITY;   // lower bound of the block's squared distances
                     if (t < nitems) {
                         int dx, dy, dz;
                         if (cube) {
-                            constexpr int W = 2 * FB_R0 + 1;
-                            dz = t / (W * W) - FB_R0;
-                            const int u = t % (W * W);
-                            dy = u / W - FB_R0;
-                            dx = u % W - FB_R0;
+                            dx = c_shell[3 * t];
+                            dy = c_shell[3 * t + 1];
+                            dz = c_shell[3 * t + 2];
                         } else {
                             int r = ra, u = t;
                             while (u >= ring_size(r)) u -= ring_size(r++);
@@ -913,6 +929,7 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                                               gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
                                               gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
                             if (lb2 * 0.9999f < t2.lim) {
+                                lb = lb2;
                                 const int bid = (bz * G.nby + by) * G.nbx + bx;
                                 a = lsm_ld(cs, size_t(bid) * LSM_BLK_CELLS);
                                 b = lsm_ld(cs, size_t(bid + 1) * LSM_BLK_CELLS);
@@ -929,12 +946,22 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                         uint32_t ra_ = __shfl(a, src, LSM_WAVE), rb_ = __shfl(b, src, LSM_WAVE);
                         float4 p = lsm_ld(G.xyz, min(ra_ + uint32_t(sub), rb_ - 1));
                         for (;;) {
-                            const bool more = mask != 0;   // uniform in the group
+                            // the next survivor still within the group leader's pruning radius
+                            // (it only shrinks; skipping a block beyond one lane's radius leaves
+                            // the merged nearest point and rho unchanged, as the first test does)
+                            const float lim0 = __shfl(t2.lim, grp * GL, LSM_WAVE);
+                            bool more = false;   // uniform in the group
+                            while (mask) {
+                                src = __ffsll((unsigned long long)mask) - 1;
+                                mask &= mask - 1;
+                                if (__shfl(lb, src, LSM_WAVE) * 0.9999f < lim0) {
+                                    more = true;
+                                    break;
+                                }
+                            }
                             uint32_t na = 0, nb = 0;
                             float4 pn = p;
                             if (more) {
-                                src = __ffsll((unsigned long long)mask) - 1;
-                                mask &= mask - 1;
                                 na = __shfl(a, src, LSM_WAVE);
                                 nb = __shfl(b, src, LSM_WAVE);
                                 pn = lsm_ld(G.xyz, min(na + uint32_t(sub), nb - 1));
