@@ -49,6 +49,7 @@ struct NNParams {
     double m_mul, m_add;   // rho margin of a search after a pass that moved the query by dq
     float direct_rc;   // warm-start distance (cells) from which a query skips the box search
     int direct_iter;   // ... once its pair has made this many updates
+    int kcold, kmax;   // box half-widths (cells): cold start, largest warm box
 };
 
 // Correspondence state of one source point, carried from pass to pass (SoA arrays):
@@ -410,13 +411,17 @@ __device__ __forceinline__ int plan_task(const TaskPlan &tp, const PairState *st
 // arithmetic, so the result does not depend on which path resolved a query.
 //
 // Box search: the cells within the warm-start radius R = sqrt(previous neighbour's distance)
-// (at most NN_KMAX cells each way), or the 5x5x5 cells around the query's cell on a cold start.
+// (at most NN_KMAX cells each way), or the 9x9x9 cells around the query's cell on a cold start.
 // Rows of cells are visited centre-out and pruned by their slab distance against the pruning
 // radius (prune2: it yields rho); inside a row the x-sorted runs are walked from the query's x.
 // A query is resolved when its best distance is provably below every unsearched point (the box
 // faces not clipped by the grid), else queued for the fallback.
 constexpr int NN_KMAX = 4;
-constexpr int NN_KCOLD = 2;   // cold start (no previous neighbour): 5x5x5 cells
+// cold start (no previous neighbour: pass 0): 9x9x9 cells. nn + fallback ms per step, C3 / C4
+// (LSM_NN_KCOLD): 1: 102.9 / 106.1; 2: 92.8 / 64.8; 3: 93.1 / 52.1; 4: 93.2 / 47.2; 5 (with
+// NN_KMAX 5): 95.3 / 47.4 -- a wider first box settles the revisit pairs' far queries (large
+// initial errors) without the fallback
+constexpr int NN_KCOLD = 4;
 // In pairs with >= NN_DIRECT_ITER updates, warm starts at least NN_DIRECT_RC cells away skip the
 // box search (nn_query). nn + fallback ms per step, C3 (1999 sequence pairs) / C4 (512 revisit
 // pairs): off 100.4 / 64.7; 3 cells from update 0: 92.5 / 93.6; from 4: 92.9 / 71.5; from 12:
@@ -479,7 +484,7 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     auto clampc = [](float f, int n) { return (int)fminf(fmaxf(floorf(f), 0.f), float(n - 1)); };
     const int cx = clampc(fx, G.nx), cy = clampc(fy, G.ny), cz = clampc(fz, G.nz);
     // box half-width in cells: the warm-start radius (+ f32 slack), else NN_KCOLD
-    int K = NN_KCOLD;
+    int K = prm.kcold;
     if (t2.bd2 < INFINITY) {
         const float rc = sqrtf(t2.bd2) * G.inv_cell * 1.0001f + 1e-4f;
         // In a pair that keeps iterating (direct_ok: >= NN_DIRECT_ITER updates, the chaotic
@@ -494,7 +499,7 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
             NN_ST(ns, 7, sub == 0 ? 1 : 0);
             return false;
         }
-        K = rc >= float(NN_KMAX) ? NN_KMAX : max(1, (int)ceilf(rc));
+        K = rc >= float(prm.kmax) ? prm.kmax : max(1, (int)ceilf(rc));
     } else {
         NN_ST(ns, 6, 1);
     }
@@ -1470,6 +1475,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         const double d = envf("LSM_NN_DIRECT", NN_DIRECT_RC);
         prm.direct_rc = d > 0.0 ? float(d) : INFINITY;
         prm.direct_iter = int(envf("LSM_NN_DIRECT_ITER", NN_DIRECT_ITER));
+        prm.kcold = std::max(1, int(envf("LSM_NN_KCOLD", NN_KCOLD)));
+        prm.kmax = std::max(1, int(envf("LSM_NN_KMAX", NN_KMAX)));
     }
 
     // Passes are launched back to back; the plan of each pass is rebuilt on the device after the
