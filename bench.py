@@ -11,8 +11,11 @@ Weak scaling: every GPU owns P pairs of one long sequence (distributed.py).
     python bench.py [--gpus N --steps K --warmup W --pairs-per-gpu P]
 
 Prints one JSON line (rank 0) with the roofline of the NN correspondence kernel (HIP events on
-the library's own stream, SURVEY.md §8d algorithmic bytes) and a CPU baseline (the C++/OpenMP f64
-implementation under oracle/cpu, rank 0 at N = 1 only, bounded sample, all threads and 1 thread).
+the library's own stream, SURVEY.md §8d algorithmic bytes), the roofline of the normals kernel
+(VALU issue from the committed PMC instruction count, and algorithmic FLOPs from the device's
+neighbourhood sizes), a CPU baseline (the C++/OpenMP f64 implementation under oracle/cpu, rank 0
+at N = 1 only, bounded sample, every usable core and 1 core) and config C1's line (8k-point P2P
+pairs: the CPU implementation, and the same pairs on the GPU).
 """
 from __future__ import annotations
 
@@ -29,6 +32,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+FP32_VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md chip-level parameters (vector)
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one 64-lane wave instruction per 2 cycles per
+# SIMD (MI355X_MICROARCH.md 'Wave scheduling'), in G wave-instructions/s
+VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 2   # = 1228.8
 KERNELS = ["filter", "grid", "normals", "nn", "nn_fallback", "accumulate",
            "solve", "voxel"]
 
@@ -44,7 +51,7 @@ def parse():
                          "ouster_multiscale: C5 256k Ouster-128, voxel 0.4/0.2/0.1 m chain; "
                          "loop_closure: C4 independent 64k revisit pairs (sharded, no halo)")
     ap.add_argument("--pairs-per-gpu", type=int, default=0,
-                    help="0: 1999 (hdl64: the C3 2000-keyframe sequence), 32 (ouster), "
+                    help="0: 1999 (hdl64: the C3 2000-keyframe sequence), 256 (ouster), "
                          "512 (loop_closure: C4's 4096 pairs over 8 GPUs)")
     ap.add_argument("--seed", type=int, default=-1, help="-1: 3 (hdl64), 5 (ouster)")
     ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
@@ -54,10 +61,14 @@ def parse():
                          "latency-bound ICP passes overlap another's normal estimation")
     ap.add_argument("--cpu-sample-pairs", type=int, default=0,
                     help="bounded CPU-baseline sample, 1/12 of it again on 1 core (0: 144 pairs "
-                         "for hdl64_seq, 72 for loop_closure, 16 for ouster_multiscale: ~10 s "
+                         "for hdl64_seq, 72 for loop_closure, 32 for ouster_multiscale: ~10 s "
                          "each on 16 cores of the GPU box's EPYC)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: every core this process may use (affinity mask, capped by the "
+                         "cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c1", action="store_true",
+                    help="skip config C1's line (8k-point P2P pairs, CPU and GPU)")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
     ap.add_argument("--seq-cache", default="",
                     help="A/B runs (hdl64_seq): load the synthetic sequence from this .npz if it "
@@ -80,6 +91,19 @@ def load_or_make_sequence(path, P, seed, model, first, procs):
     return seq
 
 
+def usable_cores() -> int:
+    """Cores this process may run on: the affinity mask, capped by a cgroup v2 CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(float(q) / float(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def _cpu_host():
     model = ""
     try:
@@ -96,7 +120,7 @@ def _cpu_host():
 def _cpu_timed(run, n_pairs: int, threads: int, what: str):
     """Time run(n) on `threads` OpenMP threads and a smaller sample on 1 thread."""
     from oracle import cpu_ref as C
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = max(1, threads)
     C.load()
     def timed(n, min_s):   # the sample again until it has run >= min_s (small workloads)
         done, t0 = 0, time.perf_counter()
@@ -116,7 +140,9 @@ def _cpu_timed(run, n_pairs: int, threads: int, what: str):
             "value_1core": round(n1 / dt1, 3),
             "sample": f"{what}: {n_all} pairs on {threads} threads ({dt:.1f} s) and {n1} on 1 "
                       f"thread ({dt1:.1f} s); the C++/OpenMP f64 KD-tree implementation of the "
-                      f"path (oracle/cpu/lsm_cpu.cpp, SURVEY.md 8d) on {model}, nproc {ncpu}"}
+                      f"path (oracle/cpu/lsm_cpu.cpp, SURVEY.md 8d) on {model}, nproc {ncpu}, "
+                      f"{len(os.sched_getaffinity(0))} in the affinity mask, {usable_cores()} "
+                      f"usable (cgroup quota)"}
 
 
 def cpu_baseline(seq, n_pairs: int, method: str, threads: int):
@@ -162,6 +188,40 @@ def cpu_baseline_pairs(seq, P: int, n_pairs: int, method: str, threads: int):
                                              "pair)")
 
 
+C1_PAIRS = 256
+
+
+def c1_line(dev, seq, threads: int, cpu_pairs: int = 96):
+    """Config C1 (BASELINE.json configs[0]): single 8k-point P2P registrations, Open3D defaults.
+    GPU: the 256 consecutive pairs of a seed-1 VLP-16 sequence as one batch (filter + ICP, no
+    normals), wall clock per batch with the batch's inputs resident; CPU: the C++ f64
+    implementation on the first pairs of the same sequence (every usable core and 1 core)."""
+    from lidar_slam_arvc_amd import _lib
+    ids = [dev.upload(s) for s in seq.scans]
+    prep = _lib.prep_params(want_normals=False)
+    icp = _lib.icp_params(method="p2p")
+    try:
+        def run():
+            dev.preprocess(ids, prep)
+            return dev.icp_batch_arrays(ids[1:], ids[:-1], seq.priors, icp)
+        run()
+        reps, t0 = 0, time.perf_counter()
+        while reps < 3 or time.perf_counter() - t0 < 1.0:
+            res = run()
+            reps += 1
+        dt = (time.perf_counter() - t0) / reps
+    finally:
+        for h in ids:
+            dev.release(h)
+    cpu = cpu_baseline(seq, min(cpu_pairs, len(seq.priors)), "p2p", threads)
+    return {"workload": "vlp16_8k_p2p_seq (BASELINE.json configs[0]: 8k-pt P2P pairs)",
+            "pairs": len(seq.priors), "points_per_scan_post_filter":
+                int(np.mean([len(s) for s in seq.scans])),
+            "gpu_value": round(len(seq.priors) / dt, 3), "gpu_ms_per_batch": round(dt * 1e3, 3),
+            "mean_icp_iterations": float(np.mean(res["iterations"])),
+            "unit": "pairs/s", "cpu_baseline": cpu}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -171,7 +231,7 @@ def main():
 
     ouster = args.workload == "ouster_multiscale"
     loop = args.workload == "loop_closure"
-    P = args.pairs_per_gpu or (32 if ouster else (512 if loop else 1999))
+    P = args.pairs_per_gpu or (256 if ouster else (512 if loop else 1999))
     first = rank * P
     model = synthetic.OUSTER128 if ouster else synthetic.HDL64
     seed = args.seed if args.seed >= 0 else (5 if ouster else (4 if loop else 3))
@@ -186,6 +246,13 @@ def main():
         del ps
     else:
         seq = load_or_make_sequence(args.seq_cache, P, seed, model, first, procs)
+    c1 = None
+    do_cpu = world == 1 and not args.no_cpu_baseline
+    if do_cpu and not args.no_c1:
+        # C1: 8k-point (16 x 512 ray) P2P pairs, seed 1 -- the reference's CPU-runnable case
+        c1 = synthetic.make_sequence(C1_PAIRS + 1, seed=1, model=synthetic.VLP16_8K,
+                                     processes=procs)
+    cpu_threads = args.cpu_threads or usable_cores()
 
     import torch
     import torch.distributed as dist
@@ -197,7 +264,7 @@ def main():
         group = dist.group.WORLD
 
     from lidar_slam_arvc_amd import _lib
-    from lidar_slam_arvc_amd.distributed import compose_global_sharded
+    from lidar_slam_arvc_amd.distributed import compose_global_sharded, gather_pair_results
 
     extra_ids = []                                   # (context, handle) of extra runs
     devs = [None]
@@ -228,8 +295,8 @@ def main():
             res = dev.icp_batch_arrays(ids[P:], ids[:P], seq.priors, icp)
             rel = res["transformation"]
             if group is not None:   # the sequence-level exchange: gather every pair's result
-                allr = [torch.empty(P, 16, dtype=torch.float64, device=cuda) for _ in range(world)]
-                dist.all_gather(allr, torch.from_numpy(rel.reshape(P, 16)).to(cuda))
+                gather_pair_results(rel, np.arange(first, first + P), world * P, group=group,
+                                    device=cuda)
             return n, res
     else:
         prep = _lib.prep_params(want_normals=want_normals, grid_cell=args.grid_cell)
@@ -300,6 +367,53 @@ def main():
 
     stats = {k: kstats(k) for k in KERNELS}
     nn = kstats("nn_pass")   # check + search + fallback of every ICP pass
+    cnt = {k: kstats(k)["launches"] for k in ("nn_uncertified", "nn_queries",
+                                              "nn_queries_first_pass", "nn_pending",
+                                              "nn_pending_first_pass")}
+    roof_n = None
+    nst = stats["normals"]
+    if want_normals and nst["launches"] and len(devs) == 1:
+        # neighbourhood sizes of the same work: one untimed pre-process in statistics mode
+        d0 = devs[0]
+        d0.reset_stats()
+        os.environ["LSM_NORMALS_STATS"] = "1"
+        try:
+            if ouster:
+                ms.preprocess(want_normals=True, grid_cell=args.grid_cell)
+                nlaunch = len(ms.scales)
+            else:
+                d0.preprocess(ids if loop else run_ids[0], prep)
+                nlaunch = 1
+        finally:
+            del os.environ["LSM_NORMALS_STATS"]
+        nb = d0.kernel_stats("normals_neighbours")["launches"] / nlaunch
+        npts = d0.kernel_stats("normals_points")["launches"] / nlaunch
+        avg_s = nst["ms"] / nst["launches"] * 1e-3
+        flops = 18.0 * nb + 150.0 * npts
+        valu = None
+        vfile = os.path.join(ROOT, "profiles", "normals_valu.json")
+        if os.path.exists(vfile) and not (ouster or loop):
+            with open(vfile) as f:
+                vj = json.load(f)
+            if vj.get("pairs_per_gpu") == P:   # PMC count of the same workload's launch
+                valu = vj.get("valu_per_launch")
+        ach = valu / avg_s / 1e9 if valu else None
+        roof_n = {"bound": "valu", "kernel": "normals_kernel (hybrid kNN-300 / r 0.3 m, "
+                                            "one launch per step)",
+                  "unit": "G wave-instructions/s",
+                  "achieved": round(ach, 2) if ach else None, "peak": VALU_ISSUE_PEAK_G,
+                  "frac": round(ach / VALU_ISSUE_PEAK_G, 5) if ach else None,
+                  "valu_instructions_per_launch": valu,
+                  "avg_launch_ms": round(avg_s * 1e3, 4), "launches": nst["launches"],
+                  "flops": {"unit": "TFLOP/s", "achieved": round(flops / avg_s / 1e12, 4),
+                            "peak": FP32_VALU_PEAK_TFLOPS,
+                            "frac": round(flops / avg_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 6),
+                            "flops_per_launch": flops,
+                            "model": "SURVEY.md 8d: 18 FLOP per neighbour (9 cumulant FMAs, "
+                                     "computed in f64) + 150 per point (covariance, "
+                                     "FastEigen3x3); neighbourhood sizes counted on the device",
+                            "points_per_launch": npts,
+                            "neighbours_per_point": round(nb / max(npts, 1), 3)}}
     n_pts, res = last
     iters = [r["iterations"] for r in res] if isinstance(res, list) else list(res["iterations"])
     out = None
@@ -323,15 +437,16 @@ def main():
                 "per_kernel_ms_per_pass": {k: round(stats[k]["ms"] / max(nn["launches"], 1), 5)
                                            for k in ("nn", "nn_fallback")}}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if do_cpu:
             ns = args.cpu_sample_pairs or (32 if ouster else (72 if loop else 144))
             ns = max(1, min(ns, P))
             if ouster:
-                cpu = cpu_baseline_multiscale(seq, ns, args.method, args.cpu_threads)
+                cpu = cpu_baseline_multiscale(seq, ns, args.method, cpu_threads)
             elif loop:
-                cpu = cpu_baseline_pairs(seq, P, ns, args.method, args.cpu_threads)
+                cpu = cpu_baseline_pairs(seq, P, ns, args.method, cpu_threads)
             else:
-                cpu = cpu_baseline(seq, ns, args.method, args.cpu_threads)
+                cpu = cpu_baseline(seq, ns, args.method, cpu_threads)
+        c1_out = c1_line(dev, c1, cpu_threads) if c1 is not None else None
         ms_step = dt / args.steps * 1e3
         out = {
             "metric": ("ICP keyframe-pair registrations/sec (256k-ray Ouster-128, multi-scale)"
@@ -372,19 +487,19 @@ def main():
                         "max_correspondence_distance": 10.0,
                         "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"}),
             "roofline": roof,
+            "roofline_normals": roof_n,
             "cpu_baseline": cpu,
+            "c1": c1_out,
             "mean_icp_iterations": float(np.mean(iters)),
             "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
                                       for k, v in stats.items() if v["launches"]},
             "nn_uncertified_fraction_after_pass0": round(
-                kstats("nn_uncertified")["launches"] /
-                max(kstats("nn_queries")["launches"] -
-                    kstats("nn_queries_first_pass")["launches"], 1), 5),
+                cnt["nn_uncertified"] /
+                max(cnt["nn_queries"] - cnt["nn_queries_first_pass"], 1), 5),
             "nn_fallback_fraction": {
-                "all_passes": round(kstats("nn_pending")["launches"] /
-                                    max(kstats("nn_queries")["launches"], 1), 5),
-                "first_pass": round(kstats("nn_pending_first_pass")["launches"] /
-                                    max(kstats("nn_queries_first_pass")["launches"], 1), 5)}
+                "all_passes": round(cnt["nn_pending"] / max(cnt["nn_queries"], 1), 5),
+                "first_pass": round(cnt["nn_pending_first_pass"] /
+                                    max(cnt["nn_queries_first_pass"], 1), 5)}
         }
         print(json.dumps(out), flush=True)
     if group is not None:

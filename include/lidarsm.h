@@ -47,7 +47,7 @@ typedef int64_t lsm_cloud;
  * voxel_down_sample keyframe.py:150-151 / :158-159 (voxel_size None -> voxel_size <= 0 here);
  * estimate_normals(KDTreeSearchParamHybrid(0.3, 300)) keyframe.py:160-162, radius from :33. */
 typedef struct {
-    double min_radius;     /* 0.5  : keep x^2+y^2 > min_radius^2 (strict)  */
+    double min_radius;     /* 0.5  : keep x^2+y^2 > min_radius^2 (strict); -inf: no lower bound */
     double max_radius;     /* 35   : keep x^2+y^2 < max_radius^2 (strict)  */
     double min_height;     /* -1.0 : keep z > min_height (strict)          */
     double max_height;     /* 50.0 : keep z < max_height (strict)          */

@@ -44,6 +44,7 @@ struct NNParams {
     int max_iter;
     double rel_fit, rel_rmse;
     int split_max;     // most lanes one uncertified query's box search is split over
+    int split_place;   // where the split groups sit in the workgroup (LSM_NN_SPLIT_PLACE)
     float m0;          // rho margin of the searches without a previous pass (see prune2)
     uint32_t lin;      // runs of at most this many points are scanned whole (no entry search)
     double m_mul, m_add;   // rho margin of a search after a pass that moved the query by dq
@@ -722,17 +723,31 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         }
         __syncthreads();
         if (threadIdx.x == 0 && total > 0) atomicAdd(searched, uint32_t(total));
-        // few queries left: L lanes per query (power of two, at most split_max)
+        // few queries left: L lanes per query (power of two, at most split_max). The loop
+        // doubles L only while the doubled groups still fit, so total * L <= NN_THREADS: every
+        // uncertified query gets a group (the groups may span all four waves). Round 2's
+        // "split-placement" probes broke exactly this bound -- a loop test of total * L <= 256
+        // (final total * L up to 512) and a 128-lane offset of groups that may need 256 lanes
+        // -- so the queries past the last lane were never searched and kept stale
+        // correspondences.
         int L = 1;
         while (L < prm.split_max && total * (2 * L) <= NN_THREADS) L *= 2;
-        const int q = int(threadIdx.x) / L;
-        if (w * LSM_WAVE >= total * L) return;   // this wave has nothing to search (no stats)
-        live = q < total;
+        // LSM_NN_SPLIT_PLACE (tests: the result must not depend on where the groups sit):
+        // 0 groups from lane 0 in query order; 1 groups end in the last wave (first group at
+        // the highest wave boundary that still fits them); 2 as 0 with the query order reversed
+        const int span = total * L;
+        const int base = prm.split_place == 1 ? ((NN_THREADS - span) / LSM_WAVE) * LSM_WAVE : 0;
+        if ((w + 1) * LSM_WAVE <= base || w * LSM_WAVE >= base + span)
+            return;   // this wave has nothing to search (no stats)
+        const int rel = int(threadIdx.x) - base;
+        int q = rel / L;
+        live = rel >= 0 && q < total;
+        if (prm.split_place == 2) q = total - 1 - q;
         if (live) {
             i = s_idx[q];
             m = s_m[q];
         }
-        const int sub = int(threadIdx.x) & (L - 1);
+        const int sub = rel & (L - 1);
         const int64_t g = P.src_off + i;
         int result = -1, a2 = -1;
         float r = 0.f;
@@ -1451,14 +1466,14 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     prm.max_iter = max_iter;
     prm.rel_fit = p.relative_fitness;
     prm.rel_rmse = p.relative_rmse;
-    static const int SPLIT_MAX = [] {   // LSM_NN_SPLIT: 1 = one lane per query
+    {   // LSM_NN_SPLIT (read per call; the tests switch it): 1 = one lane per query
         const char *e = getenv("LSM_NN_SPLIT");
-        int v = e ? atoi(e) : 8;
+        const int v = e ? atoi(e) : 8;
         int l = 1;
         while (l * 2 <= v && l < 64) l *= 2;
-        return l;
-    }();
-    prm.split_max = SPLIT_MAX;
+        prm.split_max = l;
+    }
+    prm.split_place = getenv("LSM_NN_SPLIT_PLACE") ? atoi(getenv("LSM_NN_SPLIT_PLACE")) : 0;
     auto envf = [](const char *k, double d) {
         const char *e = getenv(k);
         return e ? atof(e) : d;

@@ -989,6 +989,10 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
     hybrid_lane<G>(C, j, np, stats, lds + threadIdx.x * HSTRIDE, acc);
+    // statistics run only (LSM_NORMALS_STATS): neighbourhood sizes |kNN(max_nn) & ball(r)| -- the
+    // algorithmic work of the normals (9 cumulant FMAs per neighbour), summed
+    // over 64 counters to spread the atomics
+    if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
 }
 
 // Neighbour lists of FPFH (ComputeFPFHFeature's KDTreeSearchParamHybrid): at most `cap` per
@@ -1131,8 +1135,12 @@ int run_filter(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params
         ctx->set_error("scratch allocation failed (filter)");
         return LSM_ENOMEM;
     }
-    FilterParams fp{p.max_radius * p.max_radius, p.min_radius * p.min_radius, p.min_height,
-                    p.max_height};
+    // min_radius = -inf switches the lower radius bound off (keep-all passes over derived clouds:
+    // a point on the sensor axis, x = y = 0, still passes); any other value is squared, as the
+    // reference's r2 > min_radius ** 2 (keyframe.py:92)
+    const double minr2 = (std::isinf(p.min_radius) && p.min_radius < 0) ? -INFINITY
+                                                                         : p.min_radius * p.min_radius;
+    FilterParams fp{p.max_radius * p.max_radius, minr2, p.min_height, p.max_height};
     std::vector<uint32_t> boff_h(size_t(nfb) + 1, 0);
     if (nfb > 0) {
         hipEvent_t ev;
@@ -1470,11 +1478,14 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         np.preclass = normals_preclass();
         ctx->tic("normals", &ev);
         {
-            static const bool nstats = getenv("LSM_NORMALS_STATS") != nullptr;
+            // LSM_NORMALS_STATS (read per call): count the points that needed the kNN
+            // truncation and the neighbours of every normal (slower: statistics runs only)
+            const bool nstats = getenv("LSM_NORMALS_STATS") != nullptr;
             unsigned long long *d_ns = nullptr;
             if (nstats) {
-                d_ns = (unsigned long long *)ctx->buf("n_stats", 8 * 8);
-                LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 64, st));
+                d_ns = (unsigned long long *)ctx->buf("n_stats", 72 * 8);
+                if (!d_ns) return LSM_ENOMEM;
+                LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 72 * 8, st));
             }
             static const int G = [] {   // LSM_NORMALS_G: points per load group of the walks
                 const char *e = getenv("LSM_NORMALS_G");
@@ -1486,10 +1497,17 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
             else if (G == 8) normals_kernel<8><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
             else normals_kernel<4><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
             if (nstats) {
-                unsigned long long h = 0;
-                LSM_HIP_TRY(ctx, hipMemcpyAsync(&h, d_ns, 8, hipMemcpyDeviceToHost, st));
+                unsigned long long h[72] = {};
+                LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ns, sizeof(h), hipMemcpyDeviceToHost, st));
                 LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-                ctx->stats["normals_truncated"].launches += int64_t(h);
+                ctx->stats["normals_truncated"].launches += int64_t(h[0]);
+                unsigned long long nb = 0;
+                for (int k = 8; k < 72; ++k) nb += h[k];
+                KStat &ns = ctx->stats["normals_neighbours"];
+                ns.launches += int64_t(nb);
+                int64_t npts = 0;
+                for (int k = 0; k < K; ++k) npts += wn[k];
+                ctx->stats["normals_points"].launches += npts;
             }
         }
         ctx->toc("normals", ev);
@@ -2030,7 +2048,7 @@ int lsm_voxel_normals_run(lsm_ctx *ctx, Cloud *c, double v, Cloud *o) {
     }
     lsm_prep_params kp;
     lsm_default_prep_params(&kp);
-    kp.min_radius = 0.0;
+    kp.min_radius = -INFINITY;   // keep-all: no lower radius bound (a centroid may sit at x = y = 0)
     kp.max_radius = 1e15;
     kp.min_height = -1e15;
     kp.max_height = 1e15;
@@ -2040,9 +2058,9 @@ int lsm_voxel_normals_run(lsm_ctx *ctx, Cloud *c, double v, Cloud *o) {
     std::vector<Cloud *> one{o};
     int rc = lsm_prep_batch(ctx, one, kp, nullptr);
     if (rc) return rc;
-    if (o->n != int64_t(nvox)) {   // a centroid on the z axis (x = y = 0) fails the r > 0 filter
-        ctx->set_error("voxel_down_sample with normals: a centroid lies on the sensor axis");
-        return LSM_EINVAL;
+    if (o->n != int64_t(nvox)) {   // cannot happen with the keep-all bounds above
+        ctx->set_error("internal: voxel_down_sample with normals lost centroids");
+        return LSM_EHIP;
     }
     if ((rc = ensure_cloud_buffers(ctx, o, o->n, true))) return rc;
     if (nvox)

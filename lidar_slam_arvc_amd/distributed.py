@@ -24,6 +24,74 @@ def shard_pairs(n_pairs: int, world: int, rank: int) -> tuple[int, int]:
     return a, b
 
 
+def balance_pairs(costs, world: int) -> list:
+    """Cost-balanced packing of independent pairs over `world` ranks:
+    longest-processing-time greedy -- pairs by decreasing cost (ties by index), each to the rank
+    with the smallest load so far (ties to the lowest rank). Deterministic, so every rank
+    computes the same assignment from the same costs; every pair lands on exactly one rank.
+    Returns one ascending index array per rank.
+
+    The cost of a registration is its source size times its correspondence passes (an ICP pass
+    is one search per source point): the caller passes e.g. N_src * iterations from an earlier
+    batch of the same keyframes (loop-closure candidates recur, loopclosing.py:80-99), or N_src
+    alone when no iteration counts are known."""
+    c = np.asarray(costs, dtype=np.float64).reshape(-1)
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    order = sorted(range(len(c)), key=lambda k: (-c[k], k))
+    load = [0.0] * world
+    out = [[] for _ in range(world)]
+    for k in order:
+        r = min(range(world), key=lambda q: (load[q], q))
+        out[r].append(k)
+        load[r] += c[k]
+    return [np.asarray(sorted(v), dtype=np.int64) for v in out]
+
+
+def gather_pair_results(mine: np.ndarray, index: np.ndarray, n_total: int, group=None,
+                        device=None) -> np.ndarray:
+    """The sequence-level exchange of a sharded batch: every rank contributes
+    its pairs' results (rows of `mine`, float64, pair order `index`) and receives all
+    `n_total` rows in global pair order. One all-gather of fixed-size buffers (RCCL over xGMI
+    on GPUs, gloo on CPU); ranks with fewer pairs pad. Without a process group it returns
+    `mine` scattered into global order."""
+    import torch
+    import torch.distributed as dist
+
+    mine = np.asarray(mine, dtype=np.float64)
+    width = int(np.prod(mine.shape[1:])) if mine.ndim > 1 else 1
+    rows = mine.reshape(len(index), width)
+    if group is None and not (dist.is_available() and dist.is_initialized()):
+        out = np.zeros((n_total, width))
+        out[np.asarray(index, dtype=np.int64)] = rows
+        return out.reshape((n_total,) + mine.shape[1:])
+    world = dist.get_world_size(group)
+    dev = device if device is not None else "cpu"
+    cap = -(-n_total // world) if n_total else 0
+    counts = torch.zeros(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(counts, torch.tensor([len(index)], dtype=torch.int64, device=dev),
+                                group=group)
+    cap = max(cap, int(counts.max().item()))
+    buf = torch.zeros((cap, width + 1), dtype=torch.float64, device=dev)
+    buf[:len(index), 0] = torch.as_tensor(np.asarray(index, dtype=np.float64), device=dev)
+    buf[:len(index), 1:] = torch.as_tensor(rows, device=dev)
+    allb = torch.empty((world * cap, width + 1), dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(allb, buf, group=group)
+    allb = allb.cpu().numpy().reshape(world, cap, width + 1)
+    out = np.zeros((n_total, width))
+    seen = np.zeros(n_total, dtype=bool)
+    for r in range(world):
+        n = int(counts[r].item())
+        idx = allb[r, :n, 0].astype(np.int64)
+        if seen[idx].any():
+            raise RuntimeError("a pair was registered by two ranks")
+        seen[idx] = True
+        out[idx] = allb[r, :n, 1:]
+    if not seen.all():
+        raise RuntimeError("some pairs were registered by no rank")
+    return out.reshape((n_total,) + mine.shape[1:])
+
+
 def local_prefix(relative: np.ndarray) -> np.ndarray:
     """G[k] = R_0 R_1 ... R_k for the chunk (k = 0 .. n-1); identity-first convention below.
     The serial 4 x 4 products run in the library's host code (a NumPy loop costs ~3 us a pair)."""

@@ -338,7 +338,7 @@ class KeyFrame:
             self._planes = None
         g, ng = self._dev.split_plane(h, np.asarray(plane_model, dtype=np.float64), thresholdB)
         self._planes = (g, ng)
-        keep_all = dict(min_radius=0.0, max_radius=1e15, min_height=-1e15, max_height=1e15,
+        keep_all = dict(min_radius=-np.inf, max_radius=1e15, min_height=-1e15, max_height=1e15,
                         max_nn=ICP_PARAMETERS.max_nn_gd, want_normals=True)
         self._dev.preprocess([g], _lib.prep_params(normal_radius=self.voxel_size_normals_ground_plane,
                                                    **keep_all))
@@ -371,7 +371,10 @@ class KeyFrame:
             if kf._handle is None or kf._prep_key is None:
                 raise RuntimeError("registration needs pre-processed keyframes (pre_process)")
         init = np.asarray(initial_transform, dtype=np.float64).reshape(1, 16)
-        res = self._dev.icp_batch([other._handle], [self._handle], init, prm)[0]
+        # the reference registers pointcloud_filtered (keyframe.py:246-252): after 'fpfh' with a
+        # voxel_size that is the twice-voxelised cloud, not the keyframe's own processed cloud
+        res = self._dev.icp_batch([other._filtered_handle()], [self._filtered_handle()], init,
+                                  prm)[0]
         self.last_registration = res
         return HomogeneousMatrix(res["transformation"])
 

@@ -80,6 +80,7 @@ class KeyFrameManager:
             for kf in group:
                 kf._prep_key = key
         for kf in kfs:
+            kf._release_vn()   # as KeyFrame._run: pointcloud_filtered is the keyframe's cloud
             kf._filter = (None, None)
             kf.pointcloud_filtered = DevicePointCloud(self._dev, kf._handle, normals)
 
@@ -110,9 +111,11 @@ class KeyFrameManager:
         if len(pairs) == 0:
             return []
         prm = self.keyframes[pairs[0][0]].registration_params(_OPTION[self.method])
-        src = [self.keyframes[j]._handle for i, j in pairs]
-        tgt = [self.keyframes[i]._handle for i, j in pairs]
-        if any(h is None for h in src + tgt):
+        # pointcloud_filtered of each keyframe, as local_registration_simple registers
+        src = [self.keyframes[j]._filtered_handle() for i, j in pairs]
+        tgt = [self.keyframes[i]._filtered_handle() for i, j in pairs]
+        if any(h is None for h in src + tgt) or any(
+                self.keyframes[k]._prep_key is None for ij in pairs for k in ij):
             raise RuntimeError("registration needs loaded, pre-processed keyframes")
         init = np.stack([np.asarray(getattr(T, "array", T), dtype=np.float64) for T in Tijs])
         res = self._dev.icp_batch(src, tgt, init.reshape(-1, 16), prm)
@@ -122,13 +125,27 @@ class KeyFrameManager:
 
     # ------------------------------------------------------------------ maps (§8f row 3)
     def build_map(self, global_transforms, keyframe_sampling=10, radii=None, heights=None):
-        """Concatenate filtered (and voxelised) keyframes in the global frame; no rendering."""
-        radii = [0.5, 35.0] if radii is None else radii
-        heights = [-120.0, 120.0] if heights is None else heights
-        sampled = [global_transforms[i] for i in range(0, len(global_transforms), keyframe_sampling)]
+        """Map of every keyframe, filtered (radii 0.5-35 m, heights +-120 m by default), voxelised
+        when the keyframe has a voxel_size, moved to the global frame and concatenated
+        (keyframemanager.py:154-184); no rendering.
+
+        As the reference, keyframe i is placed with ``global_transforms[i * keyframe_sampling]``
+        (the i-th sampled transform), for every keyframe of the manager: fewer sampled transforms
+        than keyframes raises IndexError there (keyframemanager.py:176) and here. The device
+        filter and voxel passes are the registration path's own (bit-exact to the oracle); the
+        transform and the concatenation run on the host in f64, as Open3D's PointCloud.transform
+        and operator+ do."""
+        if radii is None:
+            radii = [0.5, 35.0]
+        if heights is None:
+            heights = [-120.0, 120.0]
+        sampled_transforms = [global_transforms[i]
+                              for i in range(0, len(global_transforms), keyframe_sampling)]
         out = HostPointCloud(np.zeros((0, 3)))
-        for kf, Ti in zip(self.keyframes, sampled):
+        for i in range(len(self.keyframes)):
+            kf = self.keyframes[i]
             kf.filter_radius_height(radii=radii, heights=heights)
             kf.down_sample()
-            out = out + kf.transform(Ti.array)
+            Ti = sampled_transforms[i]
+            out = out + kf.transform(getattr(Ti, "array", Ti))
         return out

@@ -144,6 +144,24 @@ def main(ref_root):
                           "edges": [[e[0], e[1], e[2], e[3].tolist()] for e in g.edges]})
     out_json["triangle_cases"] = tri_cases
 
+    # loop_closing_simple (loopclosing.py:33-56): candidates sampled with np.random.choice under
+    # np.random.seed, one canned registration per sampled candidate, one 'SM' edge each
+    simple_cases = []
+    for cur, seed, ncand in [(420, 5, 6), (560, 9, 4), (699, 2, 30), (50, 1, 6)]:
+        g = FakeGraph(list(poses[:cur + 1]), T0_gps)
+        lc = LoopClosing(g, distance_backwards=9.0, radius_threshold=2.0)
+        kfm = FakeKFM(poses, T0_gps)
+        np.random.seed(seed)
+        try:
+            lc.loop_closing_simple(cur, ncand, kfm)
+            err = None
+        except Exception as e:   # (no candidates: np.random.choice of an empty list works)
+            err = type(e).__name__
+        simple_cases.append({"current": cur, "seed": seed, "number_of_candidates": ncand,
+                             "error": err, "icp_calls": kfm.calls,
+                             "edges": [[e[0], e[1], e[2], e[3].tolist()] for e in g.edges]})
+    out_json["simple_cases"] = simple_cases
+
     # ---------------- EuRoC CSV schema ----------------
     with tempfile.TemporaryDirectory() as d:
         er = EurocReader(d)
@@ -161,7 +179,8 @@ def main(ref_root):
     np.savez_compressed(os.path.join(HERE, "reference_goldens.npz"), **out)
     with open(os.path.join(HERE, "reference_goldens.json"), "w") as f:
         json.dump(out_json, f, indent=1)
-    print("wrote", len(out), "arrays,", len(cases), "loop cases,", len(tri_cases), "triangle cases")
+    print("wrote", len(out), "arrays,", len(cases), "loop cases,", len(tri_cases),
+          "triangle cases,", len(simple_cases), "simple cases")
 
 
 if __name__ == "__main__":

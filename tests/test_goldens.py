@@ -163,3 +163,25 @@ def test_loop_closing_triangle_host_logic():
             assert np.allclose(np.array(a[3]), np.array(b[3]), rtol=0, atol=1e-12)
         # every distinct pair registered once (the reference repeats shared pairs)
         assert sorted(set(kfm.calls)) == sorted(set(map(tuple, case["icp_calls"])))
+
+
+def test_loop_closing_simple_host_logic():
+    """loop_closing_simple (loopclosing.py:33-56): the same sampled candidates, registrations and
+    'SM' edges as the reference under np.random.seed (reference-captured goldens)."""
+    from lidar_slam_arvc_amd.loopclosing import LoopClosing
+    poses = G["lc_poses"]
+    T0 = se3.HomogeneousMatrix(G["lc_T0_gps"].copy())
+    assert any(c["edges"] for c in J["simple_cases"])
+    for case in J["simple_cases"]:
+        cur = case["current"]
+        g = FakeGraph(list(poses[:cur + 1]), T0)
+        lc = LoopClosing(g, distance_backwards=9.0, radius_threshold=2.0,
+                         device=OracleCandidates())
+        kfm = FakeKFM()
+        np.random.seed(case["seed"])
+        lc.loop_closing_simple(cur, case["number_of_candidates"], kfm)
+        assert len(g.edges) == len(case["edges"])
+        for a, b in zip(g.edges, case["edges"]):
+            assert a[:3] == b[:3]
+            assert np.allclose(np.array(a[3]), np.array(b[3]), rtol=0, atol=1e-12)
+        assert sorted(set(kfm.calls)) == sorted(set(map(tuple, case["icp_calls"])))

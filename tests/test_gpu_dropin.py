@@ -131,6 +131,20 @@ def test_loop_closing_triangle_on_device(dev):
         assert [e[:3] for e in g.edges] == [e[:3] for e in case["edges"]]
 
 
+def test_loop_closing_simple_on_device(dev):
+    """loop_closing_simple with the device's candidate kernels: the reference's edges."""
+    from tests.test_goldens import FakeGraph, FakeKFM
+    G = np.load(os.path.join(HERE, "reference_goldens.npz"))
+    J = json.load(open(os.path.join(HERE, "reference_goldens.json")))
+    T0 = se3.HomogeneousMatrix(G["lc_T0_gps"].copy())
+    for case in J["simple_cases"]:
+        g = FakeGraph(list(G["lc_poses"][:case["current"] + 1]), T0)
+        lc = LoopClosing(g, distance_backwards=9.0, radius_threshold=2.0, device=dev)
+        np.random.seed(case["seed"])
+        lc.loop_closing_simple(case["current"], case["number_of_candidates"], FakeKFM())
+        assert [e[:3] for e in g.edges] == [e[:3] for e in case["edges"]]
+
+
 def test_loop_closing_real_icp_batch(dev):
     """Revisit pairs (C4-style, HDL-64) through the batched KeyFrameManager path with real ICP.
 
@@ -177,3 +191,61 @@ def test_nonconverged_pairs_agree_in_quality(dev):
     finally:
         for i in ids:
             dev.release(i)
+
+
+@pytest.mark.parametrize("voxel", [None, 0.3])
+def test_build_map_matches_oracle_chain(euroc, voxel):
+    """build_map (keyframemanager.py:154-184): per keyframe filter (radii 0.5-35 m, heights
+    +-120 m) -> voxel_down_sample (when a voxel_size is set) -> transform by the i-th sampled
+    global transform -> concatenate. The device filter / voxel passes are bit-exact to the oracle
+    and the host transform is the same f64 arithmetic, so the map is compared exactly; the
+    reference's indexing (sampled_transforms[i] for every keyframe) is kept, IndexError included."""
+    d, seq, times = euroc
+    kfm = KeyFrameManager(d, np.array(times), voxel_size=voxel)
+    for i in range(2):
+        kfm.add_keyframe(i)
+        kfm.load_pointcloud(i)
+    glob = [se3.HomogeneousMatrix(seq.poses[k].copy()) for k in range(len(seq.poses))]
+    m = kfm.build_map(glob, keyframe_sampling=2)
+    parts = []
+    for i in range(2):
+        p = O.filter_radius_height(seq.scans[i], 0.5, 35.0, -120.0, 120.0)
+        if voxel is not None:
+            p = O.voxel_down_sample(p, voxel)[1]
+        T = seq.poses[2 * i]
+        parts.append(p @ T[:3, :3].T + T[:3, 3])
+    ref = np.vstack(parts)
+    assert m.points.shape == ref.shape
+    assert np.array_equal(m.points, ref)
+    with pytest.raises(IndexError):          # 2 keyframes, 1 sampled transform
+        kfm.build_map(glob[:2], keyframe_sampling=2)
+
+
+def test_simple_registration_uses_filtered_cloud_after_fpfh(euroc):
+    """After pre_process('fpfh') with a voxel_size, pointcloud_filtered is the twice-voxelised
+    cloud (keyframe.py:193-203) and local_registration_simple registers exactly that cloud
+    (keyframe.py:246-252), the same as a registration of those points uploaded on their own."""
+    from lidar_slam_arvc_amd import _lib
+    d, seq, times = euroc
+    kfm = KeyFrameManager(d, np.array(times), voxel_size=0.2, method="fpfh")
+    for i in range(2):
+        kfm.add_keyframe(i)
+        kfm.load_pointcloud(i)
+        kfm.pre_process(i)
+    a, b = kfm.keyframes
+    assert a._vn is not None and b._vn is not None
+    T = a.local_registration_simple(b, seq.priors[0], option="pointplane")
+    dev = a._dev
+    ref = dev.icp_batch([b._vn], [a._vn], seq.priors[:1],
+                        _lib.icp_params(method="p2plane"))[0]
+    assert np.array_equal(T.array, ref["transformation"])
+    # and not the once-voxelised keyframe cloud
+    other = dev.icp_batch([b._handle], [a._handle], seq.priors[:1],
+                          _lib.icp_params(method="p2plane"))[0]
+    assert a.last_registration["n_corr"] == ref["n_corr"] != other["n_corr"]
+    # the manager's batched form registers the same clouds
+    kfm.method = "icppointplane"
+    Tb = kfm.compute_transformations([(0, 1)], [se3.HomogeneousMatrix(seq.priors[0].copy())])[0]
+    assert np.array_equal(Tb.array, T.array)
+    kfm.pre_process_batch([0, 1])            # back to the keyframe clouds: _vn released
+    assert a._vn is None and b._vn is None

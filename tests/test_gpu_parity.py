@@ -318,18 +318,27 @@ def test_certified_passes_bit_identical(dev, method, max_corr, monkeypatch):
         _release(dev, ids)
 
 
-def test_certified_split_searches_bit_identical_on_bench_sequence(dev, monkeypatch):
+@pytest.mark.parametrize("env", [{}, {"LSM_NN_SPLIT_PLACE": "1"}, {"LSM_NN_SPLIT_PLACE": "2"},
+                                 {"LSM_NN_SPLIT": "32"}, {"LSM_NN_SPLIT": "1"}])
+def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monkeypatch):
     """The bench's own data (seed-3 HDL-64 sequence), 24 pairs: enough pairs that the later
     passes leave workgroups with few uncertified queries, whose box searches are split over
-    2-8 lanes (nn_kernel, group_top2), and enough non-converging pairs to run the 30-update
+    2-8 lanes (nn_kernel, group_top3), and enough non-converging pairs to run the 30-update
     tail. Every result and the final correspondences must equal LSM_NN_NOCERT=1 (one lane per
-    query, every query searched every pass) bit for bit."""
+    query, every query searched every pass) bit for bit -- with the split groups from lane 0
+    (default), ending in the last wave, in reversed query order, up to 32 lanes per query, or
+    no split at all: where a query's group sits in the workgroup must not change its answer
+    (round 2's open "waves 2-3" finding)."""
     seq = synthetic.make_sequence(25, seed=3, model=synthetic.HDL64)
     ids = _prep(dev, seq.scans, want_normals=True)
     try:
         prm = _lib.icp_params(method="p2plane")
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         cert = dev.icp_batch(ids[1:], ids[:-1], seq.priors, prm)
         c_cert = dev.last_correspondences()
+        for k in env:
+            monkeypatch.delenv(k)
         monkeypatch.setenv("LSM_NN_NOCERT", "1")
         full = dev.icp_batch(ids[1:], ids[:-1], seq.priors, prm)
         c_full = dev.last_correspondences()
@@ -347,12 +356,17 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, monkeypat
                                  {"LSM_NN_FB_FAR": "0.75"}, {"LSM_NN_CERT_FROM": "1"},
                                  {"LSM_NN_CERT_FROM": "4"}, {"LSM_NN_DIRECT": "0"},
                                  {"LSM_NN_DIRECT": "1", "LSM_NN_DIRECT_ITER": "0"},
-                                 {"LSM_NN_DIRECT": "2.5", "LSM_NN_DIRECT_ITER": "1"}])
+                                 {"LSM_NN_DIRECT": "2.5", "LSM_NN_DIRECT_ITER": "1"},
+                                 {"LSM_NN_KCOLD": "1"}, {"LSM_NN_KCOLD": "2"},
+                                 {"LSM_NN_KMAX": "2"}, {"LSM_NN_KCOLD": "6", "LSM_NN_KMAX": "3"},
+                                 {"LSM_NN_SPLIT_PLACE": "1"}, {"LSM_NN_SPLIT_PLACE": "2"}])
 def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     """The exact 1-NN may be reached along different paths: fallback groups of 16 / 32 / 64
     lanes, the near/far fallback split, the stability check from pass 1, 2 or 4, queries with a
     far warm start sent straight to the fallback (from 1 cell in every pass, from 2.5 cells
-    after the first update, the default 3 cells after 12 updates, or never). Every choice
+    after the first update, the default 3 cells after 12 updates, or never), cold-start boxes
+    of 3^3 / 5^3 / 9^3 (default) / 13^3 cells, warm boxes capped at 2 / 3 / 4 (default) cells,
+    split groups placed anywhere in the workgroup. Every choice
     must give the same correspondences, so every result is bit-identical to the default's
     (C4-style revisit pairs: large initial errors, many fallback queries)."""
     ps = synthetic.make_revisit_pairs(6, seed=41, model=synthetic.HDL64)
@@ -413,3 +427,71 @@ def test_clone_is_independent(dev, seq8k):
         assert np.array_equal(dev.download(b), ref)
     finally:
         _release(dev, [a, b])
+
+
+# ------------------------------------------------------------------ sharding (§8e)
+def _arrays_equal(a, b):
+    for k in ("transformation", "fitness", "inlier_rmse", "iterations", "n_corr"):
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_sequence_bit_identical(dev, world):
+    """C3 sharding as bench.py runs it at N GPUs, rank after rank on one GPU: rank r generates
+    only keyframes a .. b of the seed-3 sequence (its pairs [a, b) plus the one-keyframe halo,
+    synthetic.make_sequence(first_index=a)), pre-processes them in its own context and
+    registers its pairs. Every relative transform, fitness, rmse, iteration count and
+    correspondence count must equal the unsharded batch bit for bit (run_scanmatcher.py:196-213:
+    the pairs are independent given the priors)."""
+    from lidar_slam_arvc_amd import distributed
+    n = 12
+    seq = synthetic.make_sequence(n + 1, seed=3, model=synthetic.HDL64)
+    prep, icp = _lib.prep_params(), _lib.icp_params()
+    ids = _prep(dev, seq.scans)
+    try:
+        ref = dev.icp_batch_arrays(ids[1:], ids[:-1], seq.priors, icp)
+    finally:
+        _release(dev, ids)
+    for r in range(world):
+        a, b = distributed.shard_pairs(n, world, r)
+        part = synthetic.make_sequence(b - a + 1, seed=3, model=synthetic.HDL64, first_index=a)
+        d = _lib.Device(0)                      # the rank's own context
+        try:
+            hs = [d.upload(s) for s in part.scans]
+            d.preprocess(hs, prep)
+            got = d.icp_batch_arrays(hs[1:], hs[:-1], part.priors, icp)
+            _arrays_equal(got, {k: np.asarray(v)[a:b] for k, v in ref.items()})
+        finally:
+            d.close()
+
+
+def test_balanced_loop_pairs_bit_identical(dev):
+    """C4 sharding: independent revisit pairs packed over 3 ranks by balance_pairs (cost = N_src
+    x iterations of a first batch), each rank's subset registered in its own context, then the
+    results put back in global order (gather_pair_results without a group): equal to the
+    unsharded batch bit for bit."""
+    from lidar_slam_arvc_amd import distributed
+    P = 7
+    ps = synthetic.make_revisit_pairs(P, seed=4, model=synthetic.HDL64)
+    prep, icp = _lib.prep_params(), _lib.icp_params()
+    ids = _prep(dev, ps.targets + ps.sources)
+    try:
+        ref = dev.icp_batch_arrays(ids[P:], ids[:P], ps.init, icp)
+        nsrc = np.array([dev.info(h)[1] for h in ids[P:]])
+    finally:
+        _release(dev, ids)
+    cost = nsrc * ref["iterations"]
+    parts = distributed.balance_pairs(cost, 3)
+    rows = np.zeros((P, 4, 4))
+    for mine in parts:
+        d = _lib.Device(0)
+        try:
+            hs = [d.upload(ps.targets[k]) for k in mine] + [d.upload(ps.sources[k]) for k in mine]
+            d.preprocess(hs, prep)
+            m = len(mine)
+            got = d.icp_batch_arrays(hs[m:], hs[:m], ps.init[mine], icp)
+            _arrays_equal(got, {k: np.asarray(v)[mine] for k, v in ref.items()})
+            rows += distributed.gather_pair_results(got["transformation"], mine, P)
+        finally:
+            d.close()
+    assert np.array_equal(rows, ref["transformation"])

@@ -176,3 +176,73 @@ def test_compose_global_sharded_gloo(world):
     serial = O.compose_global(rel)
     for rank, a, poses in got:
         assert np.allclose(poses, serial[a:a + len(poses)], rtol=0, atol=1e-9)
+
+
+def test_balance_pairs_covers_every_pair_once():
+    """§8e cost-balanced packing (C4/C5): LPT greedy over N_src x iterations; every pair on
+    exactly one rank, deterministic, and within one pair's cost of the mean load."""
+    rng = np.random.default_rng(5)
+    for n in [0, 1, 5, 40, 4096]:
+        iters = rng.integers(3, 31, size=n)
+        nsrc = rng.integers(40000, 65000, size=n)
+        cost = nsrc * iters
+        for w in [1, 2, 3, 8]:
+            parts = distributed.balance_pairs(cost, w)
+            assert len(parts) == w
+            allp = np.concatenate(parts) if n else np.zeros(0, dtype=np.int64)
+            assert np.array_equal(np.sort(allp), np.arange(n))
+            for p in parts:
+                assert np.array_equal(p, np.sort(p))
+            if n:
+                loads = np.array([cost[p].sum() for p in parts])
+                assert loads.max() <= cost.sum() / w + cost.max()
+            again = distributed.balance_pairs(cost, w)
+            assert all(np.array_equal(a, b) for a, b in zip(parts, again))
+    # better than contiguous equal-count shards on skewed costs
+    cost = np.r_[np.full(64, 30.0), np.full(448, 3.0)]
+    lpt = max(cost[p].sum() for p in distributed.balance_pairs(cost, 8))
+    cont = max(cost[slice(*distributed.shard_pairs(512, 8, r))].sum() for r in range(8))
+    assert lpt < 0.5 * cont
+
+
+def _gather_worker(rank, world, port, res, cost, out_q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = distributed.balance_pairs(cost, world)[rank]
+    # each rank "registers" only its pairs: here their rows of a known result table
+    allr = distributed.gather_pair_results(res[mine], mine, len(res))
+    out_q.put((rank, allr))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_pair_results_gloo(world):
+    """The C4/C5 result exchange (bench.py loop_closure, one all-gather): ranks holding
+    LPT-balanced, uneven subsets of the pairs all receive every pair's 4 x 4 result in global
+    order, bit for bit."""
+    import multiprocessing as mp
+    import socket
+    rng = np.random.default_rng(world)
+    res = rng.normal(size=(37, 4, 4))
+    cost = rng.integers(1, 100, size=37).astype(np.float64)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, res, cost, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, allr in got:
+        assert np.array_equal(allr, res)
+    # no process group: the rank's rows scattered into global order
+    idx = np.array([3, 1, 7])
+    out = distributed.gather_pair_results(res[idx], idx, 10)
+    assert np.array_equal(out[idx], res[idx]) and not out[[0, 2, 4, 5, 6, 8, 9]].any()
