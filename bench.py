@@ -145,7 +145,8 @@ def _cpu_timed(run, n_pairs: int, threads: int, what: str):
                       f"usable (cgroup quota)"}
 
 
-def cpu_baseline(seq, n_pairs: int, method: str, threads: int):
+def cpu_baseline(seq, n_pairs: int, method: str, threads: int,
+                 what: str = "consecutive pairs of the same synthetic HDL-64 sequence"):
     """The CPU implementation on the first pairs of the same sequence (P+1 keyframes pre-processed
     per P pairs, as in a GPU step)."""
     from oracle import cpu_ref as C
@@ -157,8 +158,7 @@ def cpu_baseline(seq, n_pairs: int, method: str, threads: int):
             pre.append((pts, C.estimate_normals(pts) if method == "p2plane" else None))
         for k in range(n):
             C.registration_icp(pre[k + 1][0], pre[k][0], 10.0, seq.priors[k], method, pre[k][1])
-    return _cpu_timed(run, n_pairs, threads, "consecutive pairs of the same synthetic HDL-64 "
-                                             "sequence")
+    return _cpu_timed(run, n_pairs, threads, what)
 
 
 def cpu_baseline_multiscale(seq, n_pairs: int, method: str, threads: int):
@@ -213,7 +213,8 @@ def c1_line(dev, seq, threads: int, cpu_pairs: int = 96):
     finally:
         for h in ids:
             dev.release(h)
-    cpu = cpu_baseline(seq, min(cpu_pairs, len(seq.priors)), "p2p", threads)
+    cpu = cpu_baseline(seq, min(cpu_pairs, len(seq.priors)), "p2p", threads,
+                       "consecutive pairs of the same synthetic VLP-16 (8k-ray) sequence, P2P")
     return {"workload": "vlp16_8k_p2p_seq (BASELINE.json configs[0]: 8k-pt P2P pairs)",
             "pairs": len(seq.priors), "points_per_scan_post_filter":
                 int(np.mean([len(s) for s in seq.scans])),

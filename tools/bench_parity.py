@@ -82,14 +82,56 @@ def run_cpu(seq, threads: int, log=print):
 
 
 def run_gpu(seq):
+    """The bench's batch; returns (results, device, handles) -- the handles stay resident for
+    explain()."""
     from lidar_slam_arvc_amd import _lib
     dev = _lib.device(0)
     ids = [dev.upload(s) for s in seq.scans]
     dev.preprocess(ids, _lib.prep_params())
     res = dev.icp_batch_arrays(ids[1:], ids[:-1], seq.priors, _lib.icp_params())
-    out = {k: np.array(v) for k, v in res.items()}
-    for h in ids:
-        dev.release(h)
+    return {k: np.array(v) for k, v in res.items()}, dev, ids
+
+
+def _dRdt(A, B):
+    return (float(np.abs(A[:3, :3] - B[:3, :3]).max()), float(np.abs(A[:3, 3] - B[:3, 3]).max()))
+
+
+def explain(seq, pairs, gpu, cpu, dev, ids, threads, log=print):
+    """Pairs outside the bar, three ways: the GPU, the C++ oracle and the NumPy oracle on the
+    same clouds; the target normals of the GPU against both oracles' (points whose normals
+    differ by more than 1e-6 in |cos|, with their neighbourhood sizes); and the C++ oracle's ICP
+    run with the GPU's normals, which isolates the normals' share of the difference."""
+    from oracle import cpu_ref as C
+    from oracle import open3d_restated as O
+    C.set_threads(threads)
+    out = []
+    for k in pairs:
+        tgt = C.filter_radius_height(seq.scans[k])
+        src = C.filter_radius_height(seq.scans[k + 1])
+        g_pts, g_nrm = dev.download(ids[k], normals=True)
+        assert np.array_equal(g_pts, tgt)
+        c_nrm, c_cnt = C.estimate_normals(tgt, return_counts=True)
+        p_nrm = O.estimate_normals(tgt)
+        dot_c = np.abs((g_nrm * c_nrm).sum(1))
+        dot_p = np.abs((g_nrm * p_nrm).sum(1))
+        dot_cp = np.abs((c_nrm * p_nrm).sum(1))
+        bad = np.flatnonzero(dot_c < 1 - 1e-6)
+        Tg, Tc = gpu["transformation"][k], cpu["transformation"][k]
+        r_p = O.registration_icp(src, tgt, 10.0, seq.priors[k], "p2plane", p_nrm)
+        r_cg = C.registration_icp(src, tgt, 10.0, seq.priors[k], "p2plane", g_nrm)
+        row = {"pair": int(k),
+               "gpu_vs_cpp": _dRdt(Tg, Tc), "gpu_vs_numpy": _dRdt(Tg, r_p["transformation"]),
+               "cpp_vs_numpy": _dRdt(Tc, r_p["transformation"]),
+               "cpp_icp_with_gpu_normals_vs_gpu": _dRdt(r_cg["transformation"], Tg),
+               "iters": [int(gpu["iterations"][k]), int(cpu["iterations"][k]),
+                         int(r_p["iterations"])],
+               "normals_differing_gpu_cpp": int(len(bad)),
+               "normals_differing_gpu_numpy": int((dot_p < 1 - 1e-6).sum()),
+               "normals_differing_cpp_numpy": int((dot_cp < 1 - 1e-6).sum()),
+               "neighbourhood_sizes_of_differing": sorted(int(c) for c in c_cnt[bad])[:40],
+               "points": int(len(tgt))}
+        out.append(row)
+        log(json.dumps(row), flush=True)
     return out
 
 
@@ -149,6 +191,10 @@ def main():
                     help="run the C++ oracle here instead of reading the fixture")
     ap.add_argument("--threads", type=int, default=0, help="0: every core this process may use")
     ap.add_argument("--out", default="")
+    ap.add_argument("--explain", action="store_true",
+                    help="three-way analysis (GPU / C++ / NumPy oracle, normals) of every pair "
+                         "outside the bar")
+    ap.add_argument("--save-gpu", default="", help="write the GPU's per-pair results here")
     args = ap.parse_args()
     threads = args.threads or len(os.sched_getaffinity(0))
 
@@ -164,7 +210,7 @@ def main():
               f"-> {args.make_cpu}", flush=True)
         return
 
-    gpu = run_gpu(seq)
+    gpu, dev, ids = run_gpu(seq)
     print(f"gpu: {args.pairs} pairs done", flush=True)
     if args.cpu_live:
         cpu = run_cpu(seq, threads)
@@ -179,6 +225,18 @@ def main():
     summary = compare(gpu, cpu)
     summary = {"workload": f"hdl64_64k_p2plane_seq seed {args.seed}, {args.pairs} pairs",
                "sequence_sha256": digest, "checker": src, **summary}
+    if args.explain:
+        P = len(cpu["transformation"])
+        Tg = np.asarray(gpu["transformation"]).reshape(P, 4, 4)
+        Tc = np.asarray(cpu["transformation"]).reshape(P, 4, 4)
+        far = [k for k in range(P)
+               if np.abs(Tg[k, :3, :3] - Tc[k, :3, :3]).max() > TOL_R or
+               np.abs(Tg[k, :3, 3] - Tc[k, :3, 3]).max() > TOL_T]
+        summary["outside_explained"] = explain(seq, far, gpu, cpu, dev, ids, threads)
+    if args.save_gpu:
+        np.savez_compressed(args.save_gpu, sha256=digest, **gpu)
+    for h in ids:
+        dev.release(h)
     text = json.dumps(summary, indent=1)
     print(text)
     if args.out:
