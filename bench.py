@@ -36,8 +36,8 @@ FP32_VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md chip-level parameters (vec
 # VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one 64-lane wave instruction per 2 cycles per
 # SIMD (MI355X_MICROARCH.md 'Wave scheduling'), in G wave-instructions/s
 VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 2   # = 1228.8
-KERNELS = ["filter", "grid", "normals", "nn", "nn_fallback", "accumulate",
-           "solve", "voxel"]
+KERNELS = ["filter", "grid", "normals", "normals_lazy", "normals_mark", "nn", "nn_fallback",
+           "accumulate", "solve", "voxel"]
 
 
 def parse():
@@ -55,6 +55,12 @@ def parse():
                          "512 (loop_closure: C4's 4096 pairs over 8 GPUs)")
     ap.add_argument("--seed", type=int, default=-1, help="-1: 3 (hdl64), 5 (ouster)")
     ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
+    ap.add_argument("--normals", default="auto", choices=["auto", "lazy", "eager"],
+                    help="eager: every normal of every keyframe in the pre-process; lazy "
+                         "(LSM_NORMALS_LAZY): a keyframe's normals are computed when it is first "
+                         "a P2Plane target (bit-identical registrations; sources never compute "
+                         "theirs); auto: eager for hdl64_seq (every keyframe but the last is a "
+                         "target), lazy for loop_closure and ouster_multiscale")
     ap.add_argument("--streams", type=int, default=1,
                     help="hdl64_seq: independent contexts (HIP streams) per GPU, each registering a "
                          "contiguous run of the pairs from its own host thread, so one run's "
@@ -232,6 +238,8 @@ def main():
 
     ouster = args.workload == "ouster_multiscale"
     loop = args.workload == "loop_closure"
+    if args.normals == "auto":
+        args.normals = "lazy" if (ouster or loop) else "eager"
     P = args.pairs_per_gpu or (256 if ouster else (512 if loop else 1999))
     first = rank * P
     model = synthetic.OUSTER128 if ouster else synthetic.HDL64
@@ -272,6 +280,8 @@ def main():
     dev = _lib.device(local)
     ids = [dev.upload(s) for s in seq.scans]        # raw scans resident in HBM
     want_normals = args.method == "p2plane"
+    # pre-process normals mode: "lazy" computes only the target normals the registration reads
+    wn_mode = ("lazy" if args.normals == "lazy" else True) if want_normals else False
     cuda = torch.device("cuda", local)
     ms = None
     if ouster:
@@ -279,7 +289,7 @@ def main():
         ms = MultiScaleSet(dev, ids)                 # per-scale device clones, made once
 
         def step():
-            ms.preprocess(want_normals=want_normals, grid_cell=args.grid_cell)
+            ms.preprocess(want_normals=wn_mode, grid_cell=args.grid_cell)
             stages = ms.register(list(range(1, P + 1)), list(range(P)), seq.priors,
                                  method=args.method)
             res = stages[-1]
@@ -288,7 +298,7 @@ def main():
             n = [dev.info(h)[1] for h in ms.handles[-1]]
             return n, res
     elif loop:
-        prep = _lib.prep_params(want_normals=want_normals, grid_cell=args.grid_cell)
+        prep = _lib.prep_params(want_normals=wn_mode, grid_cell=args.grid_cell)
         icp = _lib.icp_params(method=args.method)
 
         def step():
@@ -300,7 +310,7 @@ def main():
                                     device=cuda)
             return n, res
     else:
-        prep = _lib.prep_params(want_normals=want_normals, grid_cell=args.grid_cell)
+        prep = _lib.prep_params(want_normals=wn_mode, grid_cell=args.grid_cell)
         icp = _lib.icp_params(method=args.method)
         S = max(1, min(args.streams, P))
         cut = [round(k * P / S) for k in range(S + 1)]          # pair runs [cut[s], cut[s+1])
@@ -372,49 +382,51 @@ def main():
                                               "nn_queries_first_pass", "nn_pending",
                                               "nn_pending_first_pass")}
     roof_n = None
-    nst = stats["normals"]
-    if want_normals and nst["launches"] and len(devs) == 1:
-        # neighbourhood sizes of the same work: one untimed pre-process in statistics mode
+    norm_ms = stats["normals"]["ms"] + stats["normals_lazy"]["ms"]   # every normals launch
+    if want_normals and norm_ms > 0 and len(devs) == 1:
+        # neighbourhood sizes of the normals one step computes: one more (untimed) step in
+        # statistics mode (every rank runs it: the step's collectives need all ranks)
         d0 = devs[0]
         d0.reset_stats()
         os.environ["LSM_NORMALS_STATS"] = "1"
         try:
-            if ouster:
-                ms.preprocess(want_normals=True, grid_cell=args.grid_cell)
-                nlaunch = len(ms.scales)
-            else:
-                d0.preprocess(ids if loop else run_ids[0], prep)
-                nlaunch = 1
+            step()
         finally:
             del os.environ["LSM_NORMALS_STATS"]
-        nb = d0.kernel_stats("normals_neighbours")["launches"] / nlaunch
-        npts = d0.kernel_stats("normals_points")["launches"] / nlaunch
-        avg_s = nst["ms"] / nst["launches"] * 1e-3
+        nb = d0.kernel_stats("normals_neighbours")["launches"]
+        npts = d0.kernel_stats("normals_points")["launches"]
+        step_s = norm_ms / args.steps * 1e-3
         flops = 18.0 * nb + 150.0 * npts
         valu = None
         vfile = os.path.join(ROOT, "profiles", "normals_valu.json")
         if os.path.exists(vfile) and not (ouster or loop):
             with open(vfile) as f:
                 vj = json.load(f)
-            if vj.get("pairs_per_gpu") == P:   # PMC count of the same workload's launch
-                valu = vj.get("valu_per_launch")
-        ach = valu / avg_s / 1e9 if valu else None
-        roof_n = {"bound": "valu", "kernel": "normals_kernel (hybrid kNN-300 / r 0.3 m, "
-                                            "one launch per step)",
-                  "unit": "G wave-instructions/s",
+            # PMC count of the same workload and normals mode
+            if vj.get("pairs_per_gpu") == P and vj.get("normals_mode") == args.normals:
+                valu = vj.get("valu_per_step")
+        ach = valu / step_s / 1e9 if valu else None
+        roof_n = {"bound": "valu", "kernel": ("lazy_normals_kernel (the target normals each ICP "
+                                              "pass reaches)" if args.normals == "lazy" else
+                                              "normals_kernel (one launch per step)") +
+                                             ": hybrid kNN-300 / r 0.3 m",
+                  "mode": args.normals, "unit": "G wave-instructions/s",
                   "achieved": round(ach, 2) if ach else None, "peak": VALU_ISSUE_PEAK_G,
                   "frac": round(ach / VALU_ISSUE_PEAK_G, 5) if ach else None,
-                  "valu_instructions_per_launch": valu,
-                  "avg_launch_ms": round(avg_s * 1e3, 4), "launches": nst["launches"],
-                  "flops": {"unit": "TFLOP/s", "achieved": round(flops / avg_s / 1e12, 4),
+                  "valu_instructions_per_step": valu,
+                  "ms_per_step": round(step_s * 1e3, 4),
+                  "launches_per_step": (stats["normals"]["launches"] +
+                                        stats["normals_lazy"]["launches"]) / args.steps,
+                  "flops": {"unit": "TFLOP/s", "achieved": round(flops / step_s / 1e12, 4),
                             "peak": FP32_VALU_PEAK_TFLOPS,
-                            "frac": round(flops / avg_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 6),
-                            "flops_per_launch": flops,
+                            "frac": round(flops / step_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 6),
+                            "flops_per_step": flops,
                             "model": "SURVEY.md 8d: 18 FLOP per neighbour (9 cumulant FMAs, "
                                      "computed in f64) + 150 per point (covariance, "
                                      "FastEigen3x3); neighbourhood sizes counted on the device",
-                            "points_per_launch": npts,
-                            "neighbours_per_point": round(nb / max(npts, 1), 3)}}
+                            "normals_per_step": npts,
+                            "neighbours_per_normal": round(nb / max(npts, 1), 3)}}
+
     n_pts, res = last
     iters = [r["iterations"] for r in res] if isinstance(res, list) else list(res["iterations"])
     out = None
@@ -470,7 +482,7 @@ def main():
                         "rays_per_scan": 262144, "method": args.method,
                         "voxel_scales": [0.4, 0.2, 0.1],
                         "max_correspondence_distance": [2.0, 1.0, 0.5],
-                        "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"}
+                        "normals": f"hybrid r=0.3 max_nn=300, {args.normals}", "parallelism": f"dp{world}"}
                        if ouster else
                        {"workload": f"hdl64_64k_{args.method}_loop_closure_pairs",
                         "pairs_per_gpu": P, "global_pairs": world * P,
@@ -478,7 +490,7 @@ def main():
                         "rays_per_scan": 65536, "method": args.method,
                         "init": "GT (+) N(0.3 m, 3 deg yaw)",
                         "max_correspondence_distance": 10.0,
-                        "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"}
+                        "normals": f"hybrid r=0.3 max_nn=300, {args.normals}", "parallelism": f"dp{world}"}
                        if loop else
                        {"workload": f"hdl64_64k_{args.method}_seq",
                         "pairs_per_gpu": P, "global_pairs": world * P,
@@ -486,7 +498,7 @@ def main():
                         "points_per_scan_post_filter": int(np.mean(n_pts)),
                         "rays_per_scan": 65536, "method": args.method,
                         "max_correspondence_distance": 10.0,
-                        "normals": "hybrid r=0.3 max_nn=300", "parallelism": f"dp{world}"}),
+                        "normals": f"hybrid r=0.3 max_nn=300, {args.normals}", "parallelism": f"dp{world}"}),
             "roofline": roof,
             "roofline_normals": roof_n,
             "cpu_baseline": cpu,

@@ -39,6 +39,13 @@ extern "C" {
 #define LSM_P2P 0     /* TransformationEstimationPointToPoint  (keyframe.py:246-248) */
 #define LSM_P2PLANE 1 /* TransformationEstimationPointToPlane  (keyframe.py:249-252) */
 
+/* want_normals = LSM_NORMALS_LAZY: the same normals as want_normals = 1, each computed when it
+ * is first used. A P2Plane registration computes, pass by pass, only the normals of the target
+ * points its correspondences reach (the others are never read); any other use of the normals
+ * (download, FPFH, plane split, voxel_down_sample with normals) completes them first. The
+ * values are bit-identical to the eager estimate_normals (keyframe.py:160-162). */
+#define LSM_NORMALS_LAZY 2
+
 typedef struct lsm_ctx lsm_ctx;
 typedef int64_t lsm_cloud;
 
@@ -54,7 +61,8 @@ typedef struct {
     double voxel_size;     /* <= 0: no down-sample                          */
     double normal_radius;  /* 0.3                                          */
     int32_t max_nn;        /* 300                                          */
-    int32_t want_normals;  /* 1 for 'icppointplane', 0 for 'icppointpoint' */
+    int32_t want_normals;  /* 1 for 'icppointplane', 0 for 'icppointpoint';
+                            * LSM_NORMALS_LAZY: normals on demand (below)                  */
     double grid_cell;      /* spatial-hash cell edge in metres; <= 0 -> library default (0.375) */
 } lsm_prep_params;
 

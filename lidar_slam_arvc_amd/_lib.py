@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("LIDARSM_LIB") or os.path.join(
 LSM_OK = 0
 LSM_P2P = 0
 LSM_P2PLANE = 1
+LSM_NORMALS_LAZY = 2     # lsm_prep_params.want_normals: normals on demand
 
 EXPORTED = [
     "lsm_init", "lsm_free", "lsm_last_error", "lsm_version", "lsm_default_prep_params",
@@ -405,9 +406,12 @@ def device(index: int | None = None) -> Device:
 def prep_params(min_radius=0.5, max_radius=35.0, min_height=-1.0, max_height=50.0,
                 voxel_size=None, normal_radius=0.3, max_nn=300, want_normals=True,
                 grid_cell=0.0) -> PrepParams:
+    """want_normals: True / False, or "lazy" (LSM_NORMALS_LAZY: the same normals, each computed
+    when first used -- a P2Plane registration computes only those its correspondences reach)."""
+    wn = LSM_NORMALS_LAZY if want_normals == "lazy" else (1 if want_normals else 0)
     return PrepParams(float(min_radius), float(max_radius), float(min_height), float(max_height),
                       float(voxel_size) if voxel_size is not None else 0.0, float(normal_radius),
-                      int(max_nn), 1 if want_normals else 0, float(grid_cell))
+                      int(max_nn), wn, float(grid_cell))
 
 
 def icp_params(max_correspondence_distance=10.0, method="p2plane", max_iteration=30,

@@ -49,6 +49,15 @@ void *lsm_ctx::host_pinned(size_t bytes) {
     return pinned;
 }
 
+void *lsm_ctx::host_pinned_extra(size_t bytes) {
+    if (bytes > 4096) return nullptr;
+    if (!pinned2 && hipHostMalloc(&pinned2, 4096, hipHostMallocDefault) != hipSuccess) {
+        pinned2 = nullptr;
+        return nullptr;
+    }
+    return pinned2;
+}
+
 hipEvent_t lsm_ctx::get_event() {
     if (!event_pool.empty()) {
         hipEvent_t e = event_pool.back();
@@ -104,7 +113,16 @@ static void free_cloud(Cloud *c) {
     (void)hipFree(c->d_vkeys);
     (void)hipFree(c->d_prior_ref);
     (void)hipFree(c->d_fpfh);
+    (void)hipFree(c->d_nstate);
     delete c;
+}
+
+// lazy normals (LSM_NORMALS_LAZY): every use of a cloud's normals other than a P2Plane
+// registration completes the pending ones first
+static int complete_normals(lsm_ctx *ctx, Cloud *c) {
+    if (!c->lazy) return LSM_OK;
+    std::vector<Cloud *> one{c};
+    return lsm_normals_complete(ctx, one);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -169,6 +187,7 @@ int lsm_free(lsm_ctx *ctx) {
         (void)hipEventDestroy(pe.b);
     }
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->pinned2) (void)hipHostFree(ctx->pinned2);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return LSM_OK;
@@ -320,6 +339,8 @@ int lsm_split_plane(lsm_ctx *ctx, lsm_cloud cloud, const double plane[4], double
         return LSM_ESTATE;
     }
     (void)hipSetDevice(ctx->device);
+    int rc0 = complete_normals(ctx, c);
+    if (rc0) return rc0;
     Cloud *g = new Cloud(), *r = new Cloud();
     const int rc = lsm_split_plane_run(ctx, c, plane, threshold, g, r);
     if (rc != LSM_OK) {
@@ -348,6 +369,8 @@ int lsm_voxel_down_sample_normals(lsm_ctx *ctx, lsm_cloud cloud, double voxel_si
         return LSM_ESTATE;
     }
     (void)hipSetDevice(ctx->device);
+    int rc0 = complete_normals(ctx, c);
+    if (rc0) return rc0;
     Cloud *o = new Cloud();
     const int rc = lsm_voxel_normals_run(ctx, c, voxel_size, o);
     if (rc != LSM_OK) {
@@ -377,7 +400,9 @@ int lsm_fpfh(lsm_ctx *ctx, lsm_cloud cloud, double radius, int32_t max_nn, doubl
         return LSM_EINVAL;
     }
     (void)hipSetDevice(ctx->device);
-    int rc = lsm_fpfh_run(ctx, c, radius, max_nn);
+    int rc = complete_normals(ctx, c);
+    if (rc) return rc;
+    rc = lsm_fpfh_run(ctx, c, radius, max_nn);
     if (rc) return rc;
     if (features && c->n > 0) {
         LSM_HIP_TRY(ctx, hipMemcpy(features, c->d_fpfh, size_t(std::min<int64_t>(cap, c->n)) * 33 * 8,
@@ -488,6 +513,10 @@ static int check_prep(lsm_ctx *ctx, const lsm_prep_params *p) {
         ctx->set_error("filter bounds must be finite (max_radius > 0)");
         return LSM_EINVAL;
     }
+    if (p->want_normals < 0 || p->want_normals > LSM_NORMALS_LAZY) {
+        ctx->set_error("want_normals must be 0, 1 or LSM_NORMALS_LAZY");
+        return LSM_EINVAL;
+    }
     if (p->want_normals && (!(p->normal_radius > 0) || p->max_nn < 0)) {
         ctx->set_error("Invalid KDTreeSearchParamHybrid (radius <= 0 or max_nn < 0)");
         return LSM_EINVAL;
@@ -545,6 +574,10 @@ int lsm_cloud_download(lsm_ctx *ctx, lsm_cloud cloud, double *xyz, double *norma
         return LSM_ESTATE;
     }
     (void)hipSetDevice(ctx->device);
+    if (normals) {
+        const int rc = complete_normals(ctx, c);
+        if (rc) return rc;
+    }
     return lsm_download_run(ctx, c, xyz, normals, cap);
 }
 

@@ -74,6 +74,17 @@ struct FallbackItem {
     float margin;     // rho margin of this query (see prune2)
 };
 
+// Lazy normals (LSM_NORMALS_LAZY targets of a P2Plane batch): a correspondence to target point t
+// whose normal is still pending marks it needed, and flags its 256-point block, so that the
+// pass's normals step (lsm_normals_lazy_pass) computes it before accumulate reads it. Plain byte
+// stores: racing markers write the same values.
+__device__ __forceinline__ void lazy_mark(const CloudDev &G, int t, uint8_t *blkflag) {
+    if (G.nstate && t >= 0 && G.nstate[t] == 0) {
+        G.nstate[t] = 1;
+        blkflag[G.lazy_blk0 + (t >> 8)] = 1;
+    }
+}
+
 __device__ __forceinline__ bool better(float d2, int idx, float bd2, int bidx) {
     return d2 < bd2 || (d2 == bd2 && idx < bidx);
 }
@@ -608,7 +619,7 @@ __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &
                                            const CloudDev &G, int i, int64_t g,
                                            const NNParams &prm, int32_t *__restrict__ corr,
                                            int32_t *__restrict__ alt, float4 *__restrict__ cert,
-                                           float &m) {
+                                           float &m, uint8_t *blkflag) {
     const float4 s = lsm_ld(S.xyz, i);
     double x, y, z;
     transform_point(P.T, s, x, y, z);
@@ -645,6 +656,7 @@ __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &
             } else if (swap) {
                 corr[g] = sec;
                 alt[g] = prev;
+                lazy_mark(G, sec, blkflag);
             }
             return true;
         }
@@ -682,7 +694,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
           NNParams prm, int32_t *__restrict__ corr, int32_t *__restrict__ alt,
           float4 *__restrict__ cert, FallbackItem *__restrict__ queue,
           uint32_t *__restrict__ queue_n, uint32_t queue_cap, uint32_t *__restrict__ searched,
-          unsigned long long *__restrict__ stats = nullptr) {
+          uint8_t *__restrict__ blkflag, unsigned long long *__restrict__ stats = nullptr) {
     NNStat ls{};
     NNStat *ns = STATS ? &ls : nullptr;
     // one task per workgroup: the host sizes the grid from an earlier pass's plan, which only
@@ -705,7 +717,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         __shared__ float s_m[NN_THREADS];
         __shared__ int32_t s_cnt[NN_THREADS / LSM_WAVE];
         bool need = false;
-        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, alt, cert, m);
+        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, alt, cert, m, blkflag);
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         const uint64_t bm = __ballot(need);
         if (lane == 0) s_cnt[w] = __popcll(bm);
@@ -762,7 +774,10 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         if (lead) {
             corr[g] = pending ? -2 : result;
             alt[g] = pending ? -1 : a2;
-            if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
+            if (!pending) {
+                cert[g] = make_float4(qp.x, qp.y, qp.z, r);
+                lazy_mark(G, result, blkflag);
+            }
         }
         if (STATS) {
             if (sub != 0) ls.v[0] = 0;   // one search per query
@@ -786,7 +801,10 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
     if (live) {
         corr[g] = pending ? -2 : result;
         alt[g] = pending ? -1 : a2;
-        if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
+        if (!pending) {
+            cert[g] = make_float4(qp.x, qp.y, qp.z, r);
+            lazy_mark(G, result, blkflag);
+        }
     }
     if (STATS) flush_stats(ls, stats);
 }
@@ -883,7 +901,8 @@ __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
               const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
               uint32_t queue_cap, int32_t *__restrict__ corr, float4 *__restrict__ cert,
-              unsigned long long *__restrict__ fstats, float far2, int far) {
+              unsigned long long *__restrict__ fstats, float far2, int far,
+              uint8_t *__restrict__ blkflag) {
     // far = 0: the items whose box-search best is within sqrt(far2) (or all when far2 = inf);
     // far = 1: the others (expected to need wider rings: more lanes per query)
     constexpr int NG = LSM_WAVE / GL;
@@ -1025,6 +1044,7 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
             fs[5] += hit ? 1 : 0;
             corr[g] = hit ? t2.bidx : -1;
             cert[g] = make_float4(qx, qy, qz, hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound));
+            if (hit) lazy_mark(G, t2.bidx, blkflag);
         }
     }
     if (fstats && sub == 0)
@@ -1387,7 +1407,56 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
     }
     std::vector<CloudDev> cdev(uniq.size());
-    for (size_t k = 0; k < uniq.size(); ++k) cdev[k] = uniq[k]->dev;
+    for (size_t k = 0; k < uniq.size(); ++k) {
+        cdev[k] = uniq[k]->dev;
+        cdev[k].nstate = nullptr;
+        cdev[k].lazy_blk0 = 0;
+    }
+    // lazy-normal targets of a P2Plane batch (LSM_NORMALS_LAZY). Default: every pending normal
+    // of a target is computed before the first pass, in one launch of full, cell-ordered
+    // workgroups -- the clouds that are never a P2Plane target (the sources of loop-closure or
+    // multi-scale batches) never compute theirs. LSM_NORMALS_LAZY_POINTS=1 (read per call)
+    // computes, pass by pass, only the normals the correspondences reach: bit-identical, but
+    // slower on the 1999-pair sequence (41 vs 23 ms of normals per 256 pairs: the needed points
+    // are 76 % of the targets', yet their compacted waves run 1.4-2x the eager cost per wave,
+    // and each of the ~10 tail passes waits ~1 ms on a handful of dense-point waves, DESIGN.md
+    // §7). One (radius, max_nn) per batch: targets pending with other parameters are completed.
+    LazyNormals lz;
+    std::vector<int32_t> tb_off, lazy_cd;
+    std::vector<int64_t> pt_off;
+    if (p.method == LSM_P2PLANE) {
+        std::vector<char> is_tgt(uniq.size(), 0);
+        for (int64_t k = 0; k < npairs; ++k) is_tgt[size_t(ti[k])] = 1;
+        const char *lp = getenv("LSM_NORMALS_LAZY_POINTS");
+        const bool per_point = lp && atoi(lp) != 0;
+        std::vector<Cloud *> other;
+        for (size_t k = 0; k < uniq.size(); ++k) {
+            Cloud *c = uniq[k];
+            if (!is_tgt[k] || !c->lazy) continue;
+            if (!per_point) {
+                other.push_back(c);
+                continue;
+            }
+            if (lazy_cd.empty()) {
+                lz.radius = c->lazy_radius;
+                lz.max_nn = c->lazy_max_nn;
+            }
+            if (c->lazy_radius != lz.radius || c->lazy_max_nn != lz.max_nn) {
+                other.push_back(c);
+                continue;
+            }
+            cdev[k].nstate = c->d_nstate;
+            cdev[k].lazy_blk0 = lz.tb;
+            tb_off.push_back(lz.tb);
+            lazy_cd.push_back(int32_t(k));
+            pt_off.push_back(lz.npts);
+            lz.tb += int32_t((c->n + 255) / 256);
+            lz.npts += c->n;
+        }
+        if (!other.empty() && (rc = lsm_normals_complete(ctx, other))) return rc;
+        tb_off.push_back(lz.tb);
+        lz.nl = int(lazy_cd.size());
+    }
 
     // pair states; block tasks are rebuilt for the active pairs of each pass (XCD-grouped: all
     // blocks of a pair on one XCD's L2, lanes balanced by block count)
@@ -1422,6 +1491,32 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     PairState *d_ps;
     double *d_pbytes;
     if ((rc = upload(ctx, "i_cd", cdev, &d_cd))) return rc;
+    if (lz.nl > 0) {
+        int32_t *d_tboff, *d_lcd;
+        if ((rc = upload(ctx, "i_lz_off", tb_off, &d_tboff))) return rc;
+        if ((rc = upload(ctx, "i_lz_cd", lazy_cd, &d_lcd))) return rc;
+        int64_t *d_ptoff;
+        if ((rc = upload(ctx, "i_lz_pt", pt_off, &d_ptoff))) return rc;
+        lz.tb_off = d_tboff;
+        lz.lazy_cd = d_lcd;
+        lz.pt_off = d_ptoff;
+        const size_t ncnt_lz = size_t(max_iter + 2);
+        lz.blkflag = (uint8_t *)ctx->buf("i_lz_flag", size_t(lz.tb) + 1);
+        lz.list = (uint32_t *)ctx->buf("i_lz_list", size_t(lz.tb) * 4 + 4);
+        lz.counters = (uint32_t *)ctx->buf("i_lz_cnt", ncnt_lz * 8);
+        lz.cloud_cnt = (uint32_t *)ctx->buf("i_lz_ccnt", ncnt_lz * size_t(lz.nl) * 4);
+        lz.woff = (uint32_t *)ctx->buf("i_lz_woff", ncnt_lz * size_t(lz.nl + 1) * 4);
+        lz.plist = (int32_t *)ctx->buf("i_lz_plist", size_t(lz.npts) * 4 + 4);
+        if (!lz.blkflag || !lz.list || !lz.counters || !lz.cloud_cnt || !lz.woff || !lz.plist) {
+            ctx->set_error("scratch allocation failed (lazy normals)");
+            return LSM_ENOMEM;
+        }
+        LSM_HIP_TRY(ctx, hipMemsetAsync(lz.cloud_cnt, 0, ncnt_lz * size_t(lz.nl) * 4, st));
+        lz.host_count = (uint32_t *)ctx->host_pinned_extra(64);
+        if (!lz.host_count) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, hipMemsetAsync(lz.blkflag, 0, size_t(lz.tb) + 1, st));
+        LSM_HIP_TRY(ctx, hipMemsetAsync(lz.counters, 0, size_t(max_iter + 2) * 8, st));
+    }
     if ((rc = upload(ctx, "i_ps", ps, &d_ps))) return rc;
     if ((rc = upload(ctx, "i_pbytes", pbytes, &d_pbytes))) return rc;
     const size_t nsrc_tot = size_t(std::max<int64_t>(src_off, 1));
@@ -1576,16 +1671,18 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             unsigned long long *sp = d_nst + size_t(pass) * NN_NSTAT;
             if (pass < CERT_FROM || nocert)
                 nn_kernel<false, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass,
+                    lz.blkflag, sp);
             else
                 nn_kernel<true, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass,
+                    lz.blkflag, sp);
         } else if (pass < CERT_FROM || nocert)
             nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q,
-                                                          d_qn + pass, qcap, d_sqn + pass);
+                                                          d_qn + pass, qcap, d_sqn + pass, lz.blkflag);
         else
             nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q,
-                                                         d_qn + pass, qcap, d_sqn + pass);
+                                                         d_qn + pass, qcap, d_sqn + pass, lz.blkflag);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
         {
@@ -1596,18 +1693,24 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             const float far2 = FB_FAR > 0.0 ? float(FB_FAR * FB_FAR) : INFINITY;
             if (FB_LANES == 16)
                 nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst, far2, 0);
+                                                                qcap, d_corr, d_cert, fst, far2, 0,
+                                                                lz.blkflag);
             else if (FB_LANES == 32)
                 nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst, far2, 0);
+                                                                qcap, d_corr, d_cert, fst, far2, 0,
+                                                                lz.blkflag);
             else
                 nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst, far2, 0);
+                                                                qcap, d_corr, d_cert, fst, far2, 0,
+                                                                lz.blkflag);
             if (FB_LANES != 64 && FB_FAR > 0.0)
                 nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst, far2, 1);
+                                                                qcap, d_corr, d_cert, fst, far2, 1,
+                                                                lz.blkflag);
         }
         ctx->toc("nn_fallback", ev);
+        // lazy normals: the target normals this pass's correspondences reach, before accumulate
+        if (lz.nl > 0 && (rc = lsm_normals_lazy_pass(ctx, lz, d_cd, pass))) return rc;
         ctx->tic("accumulate", &ev);
         if (p.method == LSM_P2PLANE)
             accumulate_kernel<LSM_P2PLANE><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, d_corr,

@@ -976,6 +976,19 @@ int normals_preclass() {
     return (e && atoi(e) != 0) ? 0 : 1;
 }
 
+NormalParams normal_params(double radius, int max_nn) {
+    NormalParams np;
+    np.r2 = radius * radius;
+    np.r = float(radius);
+    np.r2_lo = float(np.r2 * (1.0 - 4e-6));
+    np.r2_hi = float(np.r2 * (1.0 + 4e-6));
+    np.hscale = float(double(NB8) / np.r2);
+    np.max_nn = max_nn;
+    np.dense_k = dense_k(max_nn, np.r2);
+    np.preclass = normals_preclass();
+    return np;
+}
+
 template <int G>
 __global__ void __launch_bounds__(PT_THREADS)
 normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
@@ -1009,6 +1022,202 @@ nbr_lists_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, int32_t *
     ListAcc acc{idx + size_t(j) * cap, d2 + size_t(j) * cap, count + j, cap, 0,
                 double(q.x), double(q.y), double(q.z)};
     hybrid_lane<NORMALS_G_DEFAULT>(C, j, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
+}
+
+// ------------------------------------------------------------------------------------------
+// lazy normals (LSM_NORMALS_LAZY): the normals a P2Plane ICP pass reaches, on demand
+// ------------------------------------------------------------------------------------------
+// One 256-point block of cloud C: the points whose normal is wanted (state 1 = needed this
+// pass, or every state but 2 = computed when completing) are compacted in LDS, in cell order,
+// and lanes [0, count) each compute one with the eager kernel's hybrid_lane -- so the waves stay
+// full and spatially coherent, and every normal is bit-identical to the eager one.
+template <int G>
+__device__ __forceinline__ void lazy_block(const CloudDev &C, uint8_t *nstate, int j0,
+                                           bool complete, const NormalParams &np, uint32_t *lds,
+                                           int32_t *s_idx, int32_t *s_cnt) {
+    const int j = j0 + int(threadIdx.x);
+    bool need = false;
+    if (j < C.n) {
+        const uint8_t st = nstate[j];
+        need = complete ? st != 2 : st == 1;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t bm = __ballot(need);
+    if (lane == 0) s_cnt[w] = __popcll(bm);
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < PT_THREADS / LSM_WAVE; ++q) {
+        before += q < w ? s_cnt[q] : 0;
+        total += s_cnt[q];
+    }
+    if (need) s_idx[before + __popcll(bm & ((uint64_t(1) << lane) - 1))] = j;
+    __syncthreads();
+    if (int(threadIdx.x) < total) {
+        const int jj = s_idx[threadIdx.x];
+        const float4 q = lsm_ld(C.xyz, jj);
+        CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + jj,
+                   C.prior_ref ? C.prior_ref + C.perm[jj] : nullptr};
+        hybrid_lane<G>(C, jj, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
+        nstate[jj] = 2;
+    }
+    __syncthreads();   // s_idx / s_cnt are reused by the next block
+}
+
+// the blocks flagged by this pass's correspondence search (one flag byte per 256-point block of
+// the batch's lazy targets) -> list; flags cleared for the next pass
+__global__ void __launch_bounds__(256)
+lazy_compact_kernel(uint8_t *__restrict__ blkflag, int32_t tb, uint32_t *__restrict__ list,
+                    uint32_t *__restrict__ counters) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool f = false;
+    if (i < tb) {
+        f = blkflag[i] != 0;
+        if (f) blkflag[i] = 0;
+    }
+    const uint64_t bm = __ballot(f);
+    if (!bm) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)bm) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counters, uint32_t(__popcll(bm)));
+    base = __shfl(base, leader, LSM_WAVE);
+    if (f) list[base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = uint32_t(i);
+}
+
+// The listed blocks' needed points, gathered per cloud into full waves: one wave per listed
+// block (grid-stride) appends the block's needed points, in cell order, to its cloud's region
+// of the point list (pt_off[u] .. pt_off[u] + n_u) at an offset from one atomic per block.
+// (A block-per-workgroup form left the later passes' few needed points per block to waves of
+// one or two busy lanes: 3.5x the eager cost for 76 % of the normals.)
+__global__ void __launch_bounds__(256)
+lazy_gather_kernel(const CloudDev *__restrict__ cds, const int32_t *__restrict__ tb_off,
+                   const int32_t *__restrict__ lazy_cd, const int64_t *__restrict__ pt_off, int nl,
+                   const uint32_t *__restrict__ list, const uint32_t *__restrict__ counters,
+                   uint32_t *__restrict__ cloud_cnt, int32_t *__restrict__ plist) {
+    const uint32_t nb = counters[0];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t b = wave; b < nb; b += nwaves) {
+        const int32_t e = int32_t(list[b]);
+        int lo = 0, hi = nl;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (tb_off[mid] <= e) lo = mid;
+            else hi = mid;
+        }
+        const CloudDev C = cds[lazy_cd[lo]];
+        const int j0 = (e - tb_off[lo]) * PT_THREADS;
+        bool need[PT_THREADS / LSM_WAVE];
+        uint64_t bm[PT_THREADS / LSM_WAVE];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int q = 0; q < PT_THREADS / LSM_WAVE; ++q) {
+            const int j = j0 + q * LSM_WAVE + lane;
+            need[q] = j < C.n && C.nstate[j] == 1;
+            bm[q] = __ballot(need[q]);
+            tot += uint32_t(__popcll(bm[q]));
+        }
+        if (tot == 0) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(cloud_cnt + lo, tot);
+        base = __shfl(base, 0, LSM_WAVE);
+        int32_t *out = plist + pt_off[lo] + base;
+#pragma unroll
+        for (int q = 0; q < PT_THREADS / LSM_WAVE; ++q) {
+            if (need[q]) out[__popcll(bm[q] & ((uint64_t(1) << lane) - 1))] = j0 + q * LSM_WAVE + lane;
+            out += __popcll(bm[q]);
+        }
+    }
+}
+
+// per lazy cloud: waves of 64 gathered points; exclusive prefix over the clouds (one
+// workgroup), the total for the host (counters[1])
+__global__ void __launch_bounds__(1024)
+lazy_waves_kernel(const uint32_t *__restrict__ cloud_cnt, int nl, uint32_t *__restrict__ woff,
+                  uint32_t *__restrict__ counters) {
+    __shared__ uint32_t wsum[1024 / LSM_WAVE];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t carry = 0;
+    for (int base = 0; base < nl; base += 1024) {
+        const int k = base + threadIdx.x;
+        const uint32_t v = k < nl ? (cloud_cnt[k] + LSM_WAVE - 1) / LSM_WAVE : 0;
+        uint32_t x = v;
+#pragma unroll
+        for (int off = 1; off < LSM_WAVE; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, LSM_WAVE);
+            if (lane >= off) x += y;
+        }
+        if (lane == LSM_WAVE - 1) wsum[w] = x;
+        __syncthreads();
+        uint32_t before = carry, tot = 0;
+        for (int q = 0; q < 1024 / LSM_WAVE; ++q) {
+            before += q < w ? wsum[q] : 0;
+            tot += wsum[q];
+        }
+        if (k < nl) woff[k] = before + x - v;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        woff[nl] = carry;
+        counters[1] = carry;
+    }
+}
+
+// one wave per 64 gathered points of one cloud (the cloud is wave-uniform: SGPR descriptor,
+// as the eager kernel's workgroup-uniform one); each lane computes one normal exactly as the
+// eager normals_kernel does
+__global__ void __launch_bounds__(PT_THREADS)
+lazy_normals_kernel(const CloudDev *__restrict__ cds, const int32_t *__restrict__ lazy_cd,
+                    const int64_t *__restrict__ pt_off, int nl, NormalParams np,
+                    const uint32_t *__restrict__ woff, const uint32_t *__restrict__ cloud_cnt,
+                    const int32_t *__restrict__ plist, unsigned long long *stats) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    const int lane = threadIdx.x & 63;
+    const uint32_t gw = uint32_t(__builtin_amdgcn_readfirstlane(
+        int(blockIdx.x * (PT_THREADS / LSM_WAVE) + (threadIdx.x >> 6))));
+    if (gw >= woff[nl]) return;
+    int lo = 0, hi = nl;   // the cloud u with woff[u] <= gw < woff[u + 1]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (woff[mid] <= gw) lo = mid;
+        else hi = mid;
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    const uint32_t entry = (gw - woff[lo]) * LSM_WAVE + uint32_t(lane);
+    if (entry >= cloud_cnt[lo]) return;
+    const CloudDev C = cds[lazy_cd[lo]];
+    const int j = plist[pt_off[lo] + entry];
+    const float4 q = lsm_ld(C.xyz, j);
+    CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
+               C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
+    hybrid_lane<NORMALS_G_DEFAULT>(C, j, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
+    C.nstate[j] = 2;
+    if (stats) {   // statistics runs only: neighbours and normals computed
+        atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+        atomicAdd(stats + 1, 1ull);
+    }
+}
+
+// completion: every pending normal of the listed clouds (one workgroup per 256-point segment)
+__global__ void __launch_bounds__(PT_THREADS)
+complete_normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    __shared__ int32_t s_idx[PT_THREADS];
+    __shared__ int32_t s_cnt[PT_THREADS / LSM_WAVE];
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    lazy_block<NORMALS_G_DEFAULT>(C, C.nstate, s.start, true, np, lds, s_idx, s_cnt);
+}
+
+__global__ void __launch_bounds__(PT_THREADS)
+nstate_zero_kernel(const Seg *segs, const CloudDev *cd) {
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int j = s.start + threadIdx.x;
+    if (j < C.n) C.nstate[j] = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1389,6 +1598,15 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     for (int k = 0; k < K; ++k) {
         Cloud *c = clouds[k];
         if ((rc = ensure_cloud_buffers(ctx, c, wn[k], p.want_normals != 0))) return rc;
+        if (p.want_normals == LSM_NORMALS_LAZY && (c->nstate_cap < int64_t(wn[k]) || !c->d_nstate)) {
+            (void)hipFree(c->d_nstate);
+            c->d_nstate = nullptr;
+            c->nstate_cap = std::max<int64_t>(int64_t(wn[k]), 1);
+            if (hipMalloc(&c->d_nstate, size_t(c->nstate_cap)) != hipSuccess) {
+                ctx->set_error("hipMalloc failed (lazy normal states)");
+                return LSM_ENOMEM;
+            }
+        }
         const int64_t ncells = int64_t(geo[k].ncells);
         if (c->cell_cap < ncells + 1 || !c->d_cell) {
             (void)hipFree(c->d_cell);
@@ -1466,16 +1684,16 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     ctx->toc("grid", ev);
 
     // ---------------- normals ----------------
-    if (p.want_normals && !psegs.empty()) {
-        NormalParams np;
-        np.r2 = p.normal_radius * p.normal_radius;
-        np.r = float(p.normal_radius);
-        np.r2_lo = float(np.r2 * (1.0 - 4e-6));
-        np.r2_hi = float(np.r2 * (1.0 + 4e-6));
-        np.hscale = float(double(NB8) / np.r2);
-        np.max_nn = p.max_nn;
-        np.dense_k = dense_k(p.max_nn, np.r2);
-        np.preclass = normals_preclass();
+    const bool lazy = p.want_normals == LSM_NORMALS_LAZY;
+    if (lazy && !psegs.empty()) {   // normals on demand: every point pending
+        std::vector<CloudDev> zc(cdev);
+        for (int k = 0; k < K; ++k) zc[k].nstate = clouds[k]->d_nstate;
+        CloudDev *d_zc;
+        if ((rc = upload_vec(ctx, "g_cdz", zc, &d_zc))) return rc;
+        nstate_zero_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_zc);
+    }
+    if (p.want_normals && !lazy && !psegs.empty()) {
+        const NormalParams np = normal_params(p.normal_radius, p.max_nn);
         ctx->tic("normals", &ev);
         {
             // LSM_NORMALS_STATS (read per call): count the points that needed the kNN
@@ -1523,11 +1741,112 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         c->n = wn[k];
         c->processed = true;
         c->has_normals = p.want_normals != 0;
+        c->lazy = p.want_normals == LSM_NORMALS_LAZY && wn[k] > 0;
+        c->lazy_radius = p.normal_radius;
+        c->lazy_max_nn = p.max_nn;
         c->voxelized = vox;
         c->dev = cdev[k];
         c->nonempty_cells = hne[k];
         if (n_out) n_out[k] = wn[k];
     }
+    return LSM_OK;
+}
+
+int lsm_normals_lazy_pass(lsm_ctx *ctx, const LazyNormals &lz, const CloudDev *cds, int pass) {
+    if (lz.tb <= 0 || lz.nl <= 0) return LSM_OK;
+    hipStream_t st = ctx->stream;
+    hipEvent_t ev;
+    uint32_t *cnt = lz.counters + 2 * pass;                 // [0] listed blocks, [1] waves
+    uint32_t *ccnt = lz.cloud_cnt + size_t(pass) * lz.nl;   // gathered points per cloud
+    uint32_t *woff = lz.woff + size_t(pass) * (lz.nl + 1);
+    ctx->tic("normals_mark", &ev);
+    lazy_compact_kernel<<<(lz.tb + 255) / 256, 256, 0, st>>>(lz.blkflag, lz.tb, lz.list, cnt);
+    lazy_gather_kernel<<<std::max(1, ctx->num_cus * 8), 256, 0, st>>>(
+        cds, lz.tb_off, lz.lazy_cd, lz.pt_off, lz.nl, lz.list, cnt, ccnt, lz.plist);
+    lazy_waves_kernel<<<1, 1024, 0, st>>>(ccnt, lz.nl, woff, cnt);
+    ctx->toc("normals_mark", ev);
+    // the waves' count decides the grid: one small read-back per pass (the kernels queued so
+    // far drain meanwhile; ~10-20 us against ~90 ms of ICP per step)
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(lz.host_count, cnt + 1, 4, hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    const uint32_t nw = *lz.host_count;
+    if (nw == 0) return LSM_OK;
+    const NormalParams np = normal_params(lz.radius, lz.max_nn);
+    // LSM_NORMALS_STATS (read per call): neighbourhood sizes of the normals computed
+    unsigned long long *d_ns = nullptr;
+    if (getenv("LSM_NORMALS_STATS")) {
+        d_ns = (unsigned long long *)ctx->buf("lz_stats", 72 * 8);
+        if (!d_ns) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 72 * 8, st));
+    }
+    const int wpg = PT_THREADS / LSM_WAVE;
+    ctx->tic("normals_lazy", &ev);
+    lazy_normals_kernel<<<(nw + wpg - 1) / wpg, PT_THREADS, 0, st>>>(
+        cds, lz.lazy_cd, lz.pt_off, lz.nl, np, woff, ccnt, lz.plist, d_ns);
+    ctx->toc("normals_lazy", ev);
+    ctx->stats["normals_lazy_waves"].launches += int64_t(nw);
+    if (getenv("LSM_DEBUG_LAZY")) {   // per pass: waves and kernel time (synchronous)
+        hipEvent_t a = ctx->get_event(), b = ctx->get_event();
+        LSM_HIP_TRY(ctx, hipEventRecord(a, st));
+        lazy_normals_kernel<<<(nw + wpg - 1) / wpg, PT_THREADS, 0, st>>>(
+            cds, lz.lazy_cd, lz.pt_off, lz.nl, np, woff, ccnt, lz.plist, nullptr);
+        LSM_HIP_TRY(ctx, hipEventRecord(b, st));
+        LSM_HIP_TRY(ctx, hipEventSynchronize(b));
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, a, b);
+        fprintf(stderr, "lazy pass %2d: waves %8u  (re-run) %.3f ms\n", pass, nw, ms);
+        ctx->event_pool.push_back(a);
+        ctx->event_pool.push_back(b);
+    }
+    if (d_ns) {
+        unsigned long long h[72] = {};
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ns, sizeof(h), hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        unsigned long long nbr = 0;
+        for (int k = 8; k < 72; ++k) nbr += h[k];
+        ctx->stats["normals_neighbours"].launches += int64_t(nbr);
+        ctx->stats["normals_points"].launches += int64_t(h[1]);
+    }
+    return LSM_OK;
+}
+
+int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
+    hipStream_t st = ctx->stream;
+    int rc;
+    // one pass per (radius, max_nn) of the pending clouds
+    std::vector<Cloud *> todo;
+    for (Cloud *c : clouds)
+        if (c && c->lazy && c->n > 0 && c->d_nstate && c->d_nrm) todo.push_back(c);
+    while (!todo.empty()) {
+        const double r = todo[0]->lazy_radius;
+        const int mnn = todo[0]->lazy_max_nn;
+        std::vector<Cloud *> grp, rest;
+        for (Cloud *c : todo) (c->lazy_radius == r && c->lazy_max_nn == mnn ? grp : rest).push_back(c);
+        std::vector<CloudDev> cd(grp.size());
+        std::vector<uint32_t> n(grp.size());
+        for (size_t k = 0; k < grp.size(); ++k) {
+            cd[k] = grp[k]->dev;
+            cd[k].nrm = grp[k]->d_nrm;
+            cd[k].nstate = grp[k]->d_nstate;
+            n[k] = uint32_t(grp[k]->n);
+        }
+        std::vector<Seg> segs = point_segments(n, PT_THREADS);
+        CloudDev *d_cd;
+        Seg *d_segs;
+        if ((rc = upload_vec(ctx, "lz_cd", cd, &d_cd))) return rc;
+        if ((rc = upload_vec(ctx, "lz_segs", segs, &d_segs))) return rc;
+        hipEvent_t ev;
+        ctx->tic("normals_lazy", &ev);
+        if (!segs.empty())
+            complete_normals_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(
+                d_segs, d_cd, normal_params(r, mnn));
+        ctx->toc("normals_lazy", ev);
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        LSM_HIP_TRY(ctx, hipGetLastError());
+        for (Cloud *c : grp) c->lazy = false;
+        todo.swap(rest);
+    }
+    ctx->collect_timings();
     return LSM_OK;
 }
 

@@ -495,3 +495,100 @@ def test_balanced_loop_pairs_bit_identical(dev):
         finally:
             d.close()
     assert np.array_equal(rows, ref["transformation"])
+
+
+# ------------------------------------------------------------------ lazy normals
+def _assert_batch_equal(a, b):
+    for k in ("transformation", "fitness", "inlier_rmse", "iterations", "n_corr"):
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+
+
+@pytest.mark.parametrize("per_point", [False, True])
+def test_lazy_normals_bit_identical_on_bench_sequence(dev, per_point, monkeypatch):
+    """LSM_NORMALS_LAZY (bench.py's default): each target normal is computed when a
+    correspondence first reaches it. The registrations, their correspondence sets and -- once
+    completed by the download -- every normal equal the eager pre-process bit for bit (seed-3
+    sequence, 24 pairs including non-converging ones); a second batch on the same clouds reuses
+    the computed normals and still agrees."""
+    if per_point:
+        monkeypatch.setenv("LSM_NORMALS_LAZY_POINTS", "1")
+    seq = synthetic.make_sequence(25, seed=3, model=synthetic.HDL64)
+    icp = _lib.icp_params()
+    eager = _prep(dev, seq.scans)
+    lazy = _prep(dev, seq.scans, want_normals="lazy")
+    try:
+        ref = dev.icp_batch_arrays(eager[1:], eager[:-1], seq.priors, icp)
+        c_ref = dev.last_correspondences()
+        dev.reset_stats()
+        dev.set_timing(True)
+        got = dev.icp_batch_arrays(lazy[1:], lazy[:-1], seq.priors, icp)
+        dev.set_timing(False)
+        c_got = dev.last_correspondences()
+        _assert_batch_equal(ref, got)
+        assert np.array_equal(c_ref, c_got)
+        if per_point:   # only the reached normals, pass by pass
+            waves = dev.kernel_stats("normals_lazy_waves")["launches"]
+            npts = sum(dev.info(h)[1] for h in lazy[:-1])
+            assert 0 < 64 * waves < 1.5 * npts
+        again = dev.icp_batch_arrays(lazy[1:], lazy[:-1], seq.priors, icp)
+        _assert_batch_equal(ref, again)
+        for e, l in zip(eager, lazy):
+            pe, ne = dev.download(e, normals=True)
+            pl, nl = dev.download(l, normals=True)
+            assert np.array_equal(pe, pl) and np.array_equal(ne, nl)
+    finally:
+        _release(dev, eager + lazy)
+
+
+def test_lazy_normals_revisit_pairs_and_p2p(dev, monkeypatch):
+    """C4-style revisit pairs (large initial errors: many fallback queries, which mark their
+    targets too) with lazy targets and lazy sources whose normals are never needed; P2P on lazy
+    clouds (no normals read); a batch mixing eager and lazy targets. All equal the eager runs."""
+    for per_point in ("0", "1"):
+        monkeypatch.setenv("LSM_NORMALS_LAZY_POINTS", per_point)
+        _lazy_revisit(dev)
+
+
+def _lazy_revisit(dev):
+    ps = synthetic.make_revisit_pairs(4, seed=41, model=synthetic.HDL64)
+    scans = ps.targets + ps.sources
+    eager = _prep(dev, scans)
+    lazy = _prep(dev, scans, want_normals="lazy")
+    try:
+        for m in ("p2plane", "p2p"):
+            icp = _lib.icp_params(method=m)
+            ref = dev.icp_batch_arrays(eager[4:], eager[:4], ps.init, icp)
+            got = dev.icp_batch_arrays(lazy[4:], lazy[:4], ps.init, icp)
+            _assert_batch_equal(ref, got)
+        icp = _lib.icp_params()
+        ref = dev.icp_batch_arrays(eager[4:], eager[:4], ps.init, icp)
+        mixed_t = [eager[0], lazy[1], eager[2], lazy[3]]
+        got = dev.icp_batch_arrays(lazy[4:], mixed_t, ps.init, icp)
+        _assert_batch_equal(ref, got)
+    finally:
+        _release(dev, eager + lazy)
+
+
+def test_lazy_normals_completed_for_other_uses(dev, seq64k):
+    """Every other use of the normals (FPFH, the plane split's priors, voxel_down_sample with
+    normals, download) completes the pending ones first: the same results as eager clouds."""
+    e = _prep(dev, seq64k.scans[:1])[0]
+    l = _prep(dev, seq64k.scans[:1], want_normals="lazy")[0]
+    try:
+        fe = dev.fpfh(e)
+        fl = dev.fpfh(l)
+        assert np.array_equal(fe, fl)
+        plane = np.array([0.0, 0.0, 1.0, 0.69])
+        ge, re_ = dev.split_plane(e, plane)
+        l2 = _prep(dev, seq64k.scans[:1], want_normals="lazy")[0]
+        gl, rl = dev.split_plane(l2, plane)
+        for a, b in ((ge, gl), (re_, rl)):
+            dev.preprocess([a, b], _lib.prep_params(min_radius=-np.inf, max_radius=1e15,
+                                                    min_height=-1e15, max_height=1e15))
+            assert np.array_equal(dev.download(a, normals=True)[1], dev.download(b, normals=True)[1])
+        l3 = _prep(dev, seq64k.scans[:1], want_normals="lazy")[0]
+        ve, vl = dev.voxel_normals(e, 0.2), dev.voxel_normals(l3, 0.2)
+        assert np.array_equal(dev.download(ve, normals=True)[1], dev.download(vl, normals=True)[1])
+        _release(dev, [ge, re_, gl, rl, l2, l3, ve, vl])
+    finally:
+        _release(dev, [e, l])

@@ -24,15 +24,20 @@ for line in open(os.path.join(out, "sq.log")):
     if line.startswith("{"):
         bench = json.loads(line)
 n = len(per)
-avg = {c: sum(v.get(c, 0.0) for v in per.values()) / max(n, 1)
+# the profiled run executes warmup + steps timed steps and one statistics step (bench.py's
+# roofline_normals), each with the same normals work
+nsteps = (bench["steps"] + bench["warmup"] + 1) if bench else 1
+tot = {c: sum(v.get(c, 0.0) for v in per.values())
        for c in sorted({c for v in per.values() for c in v})}
+mode = bench["config"]["normals"].split(", ")[-1] if bench else None
 print(json.dumps({
-    "kernel": "normals_kernel (one launch per step: every keyframe of the batch)",
+    "kernel": "every normals launch of a step (normals_kernel eager; lazy_normals_kernel per "
+              "ICP pass when lazy)",
     "source": "rocprofv3 --kernel-trace --pmc SQ_* (one pass), bench.py --steps 2 --warmup 1, "
               "default workload (tools/pmc_normals_bench.sh)",
-    "dispatches": n,
+    "dispatches": n, "steps_profiled": nsteps, "normals_mode": mode,
     "pairs_per_gpu": bench["config"].get("pairs_per_gpu") if bench else None,
-    "per_launch": avg,
-    "valu_per_launch": avg.get("SQ_INSTS_VALU"),
-    "valu_per_wave": avg.get("SQ_INSTS_VALU", 0.0) / max(avg.get("SQ_WAVES", 1.0), 1.0),
+    "per_step": {c: v / nsteps for c, v in tot.items()},
+    "valu_per_step": tot.get("SQ_INSTS_VALU", 0.0) / nsteps,
+    "valu_per_wave": tot.get("SQ_INSTS_VALU", 0.0) / max(tot.get("SQ_WAVES", 1.0), 1.0),
 }, indent=1))
