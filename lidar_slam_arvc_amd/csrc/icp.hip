@@ -522,16 +522,25 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
     const uint32_t *cs = G.cell_start;
     const int W = 2 * K + 1;
+    // Rows are visited centre-out (offsets 0, -1, 1, -2, 2, ...: |offset| never decreases) and
+    // a row at offset d in z (or y) is at least (|d| - 1) cells from the query's slab. Once that
+    // bound reaches the pruning radius (which only shrinks) every later row of the loop would
+    // be skipped as well, so the loop stops there: the same rows are walked, without iterating
+    // over the pruned rest of a 9 x 9 cold box.
 #pragma unroll 1
     for (int iz = 0; iz < W; ++iz) {
-        const int dz = (iz & 1) ? -((iz + 1) >> 1) : (iz >> 1);   // 0, -1, 1, -2, 2 ...
+        const int adz = (iz + 1) >> 1;
+        if (adz >= 2 && float((adz - 1) * (adz - 1)) * c2 >= t2.lim) break;
+        const int dz = (iz & 1) ? -adz : adz;   // 0, -1, 1, -2, 2 ...
         const int z = cz + dz;
         if (z < z0 || z > z1) continue;
         const float wz = slab_cells2(fz, z) * c2;
         if (wz >= t2.lim) continue;
 #pragma unroll 1
         for (int iy = (sub - iz * W) & (L - 1); iy < W; iy += L) {   // rows t == sub (mod L)
-            const int dy = (iy & 1) ? -((iy + 1) >> 1) : (iy >> 1);
+            const int ady = (iy + 1) >> 1;
+            if (ady >= 2 && wz + float((ady - 1) * (ady - 1)) * c2 >= t2.lim) break;
+            const int dy = (iy & 1) ? -ady : ady;
             const int y = cy + dy;
             if (y < y0 || y > y1) continue;
             const float wyz = wz + slab_cells2(fy, y) * c2;

@@ -664,7 +664,11 @@ __device__ __forceinline__ void scan_run_pred(const float4 *xyz, uint32_t a, uin
 constexpr int NB8 = 128;          // level-0 bins (u8 counters)
 constexpr int NB32 = 32;          // refinement bins (u32 counters)
 constexpr int HSTRIDE = 33;       // LDS words per lane: 128 u8 / 32 u32 bins, padded to odd
-constexpr int SEL_CAP = 11;       // 3 words per (d2, index) entry -> 33 <= HSTRIDE
+// members collected by the final pass: 2 words per entry (the f32 rounding of the exact f64 d2,
+// a monotone key, and the index; f32 ties are ordered by recomputing the exact f64 d2), so 16
+// fit a lane's row. A chosen bin holding more needs a refine scan: 1.1 % of the dense points
+// of a bench scan with 11 entries (3 words: f64 d2 + index), 0.02 % with 16 (numpy study)
+constexpr int SEL_CAP = 16;
 constexpr int MAX_REFINE = 32;    // d2 levels (~11 x 5 bits) then index levels (<= 7 x 5 bits)
 
 // search radius covering every point with d2 < hi (slack for the f32 cell arithmetic)
@@ -765,9 +769,21 @@ __device__ __forceinline__ bool predict_dense(const CloudDev &C, const NormalPar
     return float(lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l)) >= np.dense_k * C.cell * C.cell;
 }
 
-template <int G, typename Acc>
+// Phase statistics of hybrid_lane (diagnostics, normals_phase_kernel only): per lane, walk steps
+// (loaded points inside the row windows) and members in scan 1, the refine scans and the final
+// pass, and whether the lane needed the kNN truncation.
+struct NPhase {
+    uint32_t v[8];   // s1 steps, s1 members, refine steps, final steps, final added, dense, refines, predicted dense
+};
+#define NP_ST(ph, c, x)              \
+    do {                             \
+        if (PH) (ph)->v[c] += (x);   \
+    } while (0)
+
+template <int G, typename Acc, bool PH = false>
 __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
-                            unsigned long long *stats, uint32_t *H, Acc &acc) {
+                            unsigned long long *stats, uint32_t *H, Acc &acc,
+                            NPhase *ph = nullptr) {
     uint8_t *H8 = reinterpret_cast<uint8_t *>(H);
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
@@ -779,6 +795,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // Dense-predicted points skip acc.add in scan 1 (histogram only); a wrong guess costs one
     // plain rescan below, which visits the ball in scan 1's order (identical sums).
     const bool dense = predict_dense(C, np, qf);
+    NP_ST(ph, 7, dense ? 1u : 0u);
     // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
     // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
     // f32 d^2 and the scale are within 4.2e-7 relative, t < 128). The rest (the sphere's
@@ -786,6 +803,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // f64 binning of the later scans implies.
     ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+            NP_ST(ph, 0, in ? 1u : 0u);
             const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
             const float f = dx * dx + dy * dy + dz * dz;
             const float t = f * np.hscale;
@@ -797,6 +815,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                 if (o.d2 < np.r2) bb = sel_level_bin(S, o.d2, k);
             }
             if (bb >= 0) {
+                NP_ST(ph, 1, 1u);
                 if (!dense) acc.add(p, k);
                 ++count;
                 lds_add(H + (bb >> 2), 1u << ((bb & 3) << 3));   // u8 bin, carries detected below
@@ -814,6 +833,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         need = 0;
     } else {
         if (!dense) acc.reset();
+        NP_ST(ph, 5, 1u);
         if (stats) atomicAdd(stats, 1ull);   // points that needed the kNN truncation
         // A u8 bin that passed 255 carried into its neighbour byte (or out of its word): each
         // such carry lowers the bin total by 255 or 256, so the total tells.
@@ -829,6 +849,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     }
     // rescan the members of the current state: their key extremes and a histogram by `next`
     auto refine = [&](const Sel &next, double &dmin, double &dmax, uint32_t &kmin, uint32_t &kmax) {
+        NP_ST(ph, 6, 1u);
 #pragma unroll
         for (int b = 0; b < NB32; ++b) H[b] = 0;
         dmin = INFINITY;
@@ -837,6 +858,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         kmax = 0u;
         ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
             scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+                NP_ST(ph, 2, in ? 1u : 0u);
                 Off o;
                 if (in && in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
                     lds_add(H + sel_level_bin(next, o.d2, k), 1u);
@@ -918,9 +940,11 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     uint32_t m = 0;
     ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+            NP_ST(ph, 3, in ? 1u : 0u);
             const float fd = f32_d2(qf, p);
             if (!in || fd > np.r2_hi || fd > above32) return;
             if (fd < below32) {
+                NP_ST(ph, 4, 1u);
                 acc.add(p, k);
                 return;
             }
@@ -928,13 +952,12 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
             if (fd >= np.r2_lo && !(o.d2 < np.r2)) return;
             const int cl = sel_classify(S, o.d2, k);
             if (cl < 0) {
+                NP_ST(ph, 4, 1u);
                 acc.add(p, k);
             } else if (cl == 0) {
                 if (m < SEL_CAP) {
-                    const uint64_t bits = __double_as_longlong(o.d2);
-                    H[3 * m] = uint32_t(bits);
-                    H[3 * m + 1] = uint32_t(bits >> 32);
-                    H[3 * m + 2] = k;
+                    H[2 * m] = __float_as_uint(float(o.d2));
+                    H[2 * m + 1] = k;
                 }
                 ++m;
             }
@@ -942,13 +965,22 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     });
     const uint32_t mm = m < SEL_CAP ? m : SEL_CAP;
     for (uint32_t e = 0; e < mm; ++e) {
-        const uint64_t be = uint64_t(H[3 * e]) | (uint64_t(H[3 * e + 1]) << 32);
-        const uint32_t ke = H[3 * e + 2];
+        const uint32_t fe = H[2 * e];   // non-negative floats order like their bit patterns
+        const uint32_t ke = H[2 * e + 1];
         uint32_t rank = 0;
+        double de = -1.0;   // exact d2 of e, computed at its first f32 tie
         for (uint32_t g = 0; g < mm; ++g) {
-            const uint64_t bg = uint64_t(H[3 * g]) | (uint64_t(H[3 * g + 1]) << 32);
-            // positive doubles order like their bit patterns
-            rank += (bg < be || (bg == be && H[3 * g + 2] < ke)) ? 1u : 0u;
+            const uint32_t fg = H[2 * g];
+            if (fg < fe) {
+                ++rank;
+            } else if (fg == fe && g != e) {
+                // f32 keys tie: the exact (d2, index) order (the f32 rounding is monotone, so
+                // distinct keys already order like the exact distances)
+                const uint32_t kg = H[2 * g + 1];
+                if (de < 0.0) de = make_off(lsm_ld(C.xyz, ke), qx, qy, qz).d2;
+                const double dg = make_off(lsm_ld(C.xyz, kg), qx, qy, qz).d2;
+                rank += (dg < de || (dg == de && kg < ke)) ? 1u : 0u;
+            }
         }
         if (rank < need) acc.add(lsm_ld(C.xyz, ke), ke);
     }
@@ -1006,6 +1038,37 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     // algorithmic work of the normals (9 cumulant FMAs per neighbour), summed
     // over 64 counters to spread the atomics
     if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+}
+
+// normals_kernel with phase statistics (LSM_NORMALS_PHASES=1, diagnostics): per counter the
+// lane sum (out[c]) and the per-wave maximum summed over waves (out[8 + c]: the wave's cost
+// under divergence)
+__global__ void __launch_bounds__(PT_THREADS)
+normals_phase_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
+                     unsigned long long *out) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int j = s.start + threadIdx.x;
+    NPhase ph{};
+    if (j < C.n) {
+        const float4 q = lsm_ld(C.xyz, j);
+        CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
+                   C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
+        hybrid_lane<NORMALS_G_DEFAULT, CumAcc, true>(C, j, np, nullptr, lds + threadIdx.x * HSTRIDE,
+                                                     acc, &ph);
+    }
+    for (int c = 0; c < 8; ++c) {
+        uint32_t sum = ph.v[c], mx = ph.v[c];
+        for (int off = 32; off > 0; off >>= 1) {
+            sum += __shfl_xor(sum, off, LSM_WAVE);
+            mx = max(mx, __shfl_xor(mx, off, LSM_WAVE));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(out + c, (unsigned long long)sum);
+            atomicAdd(out + 8 + c, (unsigned long long)mx);
+        }
+    }
 }
 
 // Neighbour lists of FPFH (ComputeFPFHFeature's KDTreeSearchParamHybrid): at most `cap` per
@@ -1710,6 +1773,24 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 return e ? atoi(e) : NORMALS_G_DEFAULT;
             }();
             const dim3 ng(unsigned(psegs.size()));
+            if (getenv("LSM_NORMALS_PHASES")) {   // diagnostics: phase statistics to stderr
+                unsigned long long *d_ph = (unsigned long long *)ctx->buf("n_phase", 16 * 8);
+                if (!d_ph) return LSM_ENOMEM;
+                LSM_HIP_TRY(ctx, hipMemsetAsync(d_ph, 0, 16 * 8, st));
+                normals_phase_kernel<<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ph);
+                unsigned long long h[16];
+                LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ph, sizeof(h), hipMemcpyDeviceToHost, st));
+                LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+                int64_t npts = 0;
+                for (int k = 0; k < K; ++k) npts += wn[k];
+                const char *nm[8] = {"s1_steps", "s1_members", "refine_steps", "final_steps",
+                                     "final_added", "dense", "refines", "pred_dense"};
+                fprintf(stderr, "normals phases over %lld points (lane sum / point, wave max sum / point):\n",
+                        (long long)npts);
+                for (int c = 0; c < 8; ++c)
+                    fprintf(stderr, "  %-13s %10.3f %10.3f\n", nm[c], double(h[c]) / double(npts),
+                            double(h[8 + c]) * 64.0 / double(npts));
+            }
             if (G == 1) normals_kernel<1><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
             else if (G == 2) normals_kernel<2><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
             else if (G == 8) normals_kernel<8><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
