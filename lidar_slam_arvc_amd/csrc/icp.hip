@@ -314,6 +314,7 @@ __device__ __forceinline__ float slab_cells2(float f, int k) {
     return d * d;
 }
 
+
 // ------------------------------------------------------------------------------------------
 // device-side work plan: the blocks of the pairs still iterating, balanced over the XCDs
 // ------------------------------------------------------------------------------------------
@@ -554,6 +555,9 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
                 xa = max(xa, (int)floorf(fx - ch));
                 xb = min(xb, (int)floorf(fx + ch));
             }
+            // The row's block parts left to right. (Centre-out with the far parts pruned by
+            // their x-slab -- fewer entry searches in the cold pass 0 -- measured slower: nn
+            // 81.7 -> 91.3 ms per step, 88.5 with the registers capped back to 7 waves/SIMD.)
             int x = xa;
             while (x <= xb) {
                 const int xe = min(xb, x | (LSM_BLK - 1));   // end of this block's row part
@@ -697,8 +701,14 @@ __device__ __forceinline__ void flush_stats(const NNStat &ls, unsigned long long
     }
 }
 
+// LSM_NN_WPE=<w>: cap the correspondence kernel's registers for w waves per SIMD (A/B builds)
+#ifdef LSM_NN_WPE
+#define LSM_NN_ATTR __attribute__((amdgpu_waves_per_eu(LSM_NN_WPE)))
+#else
+#define LSM_NN_ATTR
+#endif
 template <bool CHECK, bool STATS = false>
-__global__ void __launch_bounds__(NN_THREADS)
+__global__ void __launch_bounds__(NN_THREADS) LSM_NN_ATTR
 nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
           NNParams prm, int32_t *__restrict__ corr, int32_t *__restrict__ alt,
           float4 *__restrict__ cert, FallbackItem *__restrict__ queue,
