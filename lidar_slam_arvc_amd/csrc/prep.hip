@@ -1097,7 +1097,8 @@ nbr_lists_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, int32_t *
 template <int G>
 __device__ __forceinline__ void lazy_block(const CloudDev &C, uint8_t *nstate, int j0,
                                            bool complete, const NormalParams &np, uint32_t *lds,
-                                           int32_t *s_idx, int32_t *s_cnt) {
+                                           int32_t *s_idx, int32_t *s_cnt,
+                                           unsigned long long *stats = nullptr) {
     const int j = j0 + int(threadIdx.x);
     bool need = false;
     if (j < C.n) {
@@ -1123,6 +1124,10 @@ __device__ __forceinline__ void lazy_block(const CloudDev &C, uint8_t *nstate, i
                    C.prior_ref ? C.prior_ref + C.perm[jj] : nullptr};
         hybrid_lane<G>(C, jj, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
         nstate[jj] = 2;
+        if (stats) {   // statistics runs only: neighbours and normals computed
+            atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+            atomicAdd(stats + 1, 1ull);
+        }
     }
     __syncthreads();   // s_idx / s_cnt are reused by the next block
 }
@@ -1266,13 +1271,14 @@ lazy_normals_kernel(const CloudDev *__restrict__ cds, const int32_t *__restrict_
 
 // completion: every pending normal of the listed clouds (one workgroup per 256-point segment)
 __global__ void __launch_bounds__(PT_THREADS)
-complete_normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np) {
+complete_normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
+                        unsigned long long *stats) {
     __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
     __shared__ int32_t s_idx[PT_THREADS];
     __shared__ int32_t s_cnt[PT_THREADS / LSM_WAVE];
     const Seg s = segs[blockIdx.x];
     const CloudDev C = cd[s.cloud];
-    lazy_block<NORMALS_G_DEFAULT>(C, C.nstate, s.start, true, np, lds, s_idx, s_cnt);
+    lazy_block<NORMALS_G_DEFAULT>(C, C.nstate, s.start, true, np, lds, s_idx, s_cnt, stats);
 }
 
 __global__ void __launch_bounds__(PT_THREADS)
@@ -1916,14 +1922,29 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
         Seg *d_segs;
         if ((rc = upload_vec(ctx, "lz_cd", cd, &d_cd))) return rc;
         if ((rc = upload_vec(ctx, "lz_segs", segs, &d_segs))) return rc;
+        // LSM_NORMALS_STATS (read per call): neighbourhood sizes of the normals computed
+        unsigned long long *d_ns = nullptr;
+        if (getenv("LSM_NORMALS_STATS")) {
+            d_ns = (unsigned long long *)ctx->buf("lz_stats", 72 * 8);
+            if (!d_ns) return LSM_ENOMEM;
+            LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 72 * 8, st));
+        }
         hipEvent_t ev;
         ctx->tic("normals_lazy", &ev);
         if (!segs.empty())
             complete_normals_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(
-                d_segs, d_cd, normal_params(r, mnn));
+                d_segs, d_cd, normal_params(r, mnn), d_ns);
         ctx->toc("normals_lazy", ev);
         LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
         LSM_HIP_TRY(ctx, hipGetLastError());
+        if (d_ns) {
+            unsigned long long h[72] = {};
+            LSM_HIP_TRY(ctx, hipMemcpy(h, d_ns, sizeof(h), hipMemcpyDeviceToHost));
+            unsigned long long nbr = 0;
+            for (int k = 8; k < 72; ++k) nbr += h[k];
+            ctx->stats["normals_neighbours"].launches += int64_t(nbr);
+            ctx->stats["normals_points"].launches += int64_t(h[1]);
+        }
         for (Cloud *c : grp) c->lazy = false;
         todo.swap(rest);
     }
