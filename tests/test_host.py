@@ -246,3 +246,17 @@ def test_gather_pair_results_gloo(world):
     idx = np.array([3, 1, 7])
     out = distributed.gather_pair_results(res[idx], idx, 10)
     assert np.array_equal(out[idx], res[idx]) and not out[[0, 2, 4, 5, 6, 8, 9]].any()
+
+
+def test_host_code_under_asan_ubsan():
+    """the host code (the C++/OpenMP CPU implementation and the library's host-only
+    SE(3) prefix) built with -fsanitize=address,undefined and exercised end to end, error cases
+    included (tests/asan)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "tests", "asan")], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", OMP_NUM_THREADS="2")
+    r = subprocess.run([os.path.join(root, "oracle", "_build", "asan_host")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "asan ok" in r.stdout

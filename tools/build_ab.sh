@@ -5,7 +5,7 @@ set -eu
 NAME=$1; shift
 D=$(mktemp -d); mkdir -p lidar_slam_arvc_amd/_lib/ab
 cd lidar_slam_arvc_amd/csrc
-for f in api.cpp prep.hip icp.hip loop.hip plane.hip; do
+for f in api.cpp se3_host.cpp prep.hip icp.hip loop.hip plane.hip; do
   X=""; [ "${f##*.}" = cpp ] && X="-x hip"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" $X -c $f -o $D/$f.o &
 done
