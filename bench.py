@@ -65,6 +65,9 @@ def parse():
                     help="hdl64_seq: independent contexts (HIP streams) per GPU, each registering a "
                          "contiguous run of the pairs from its own host thread, so one run's "
                          "latency-bound ICP passes overlap another's normal estimation")
+    ap.add_argument("--stagger", action="store_true",
+                    help="with --streams S: run k starts its pre-processing when run k - 1's "
+                         "ends, so each chunk's registration overlaps the next chunk's normals")
     ap.add_argument("--cpu-sample-pairs", type=int, default=0,
                     help="bounded CPU-baseline sample, 1/12 of it again on 1 core (0: 144 pairs "
                          "for hdl64_seq, 72 for loop_closure, 32 for ouster_multiscale: ~10 s "
@@ -73,6 +76,9 @@ def parse():
                     help="0: every core this process may use (affinity mask, capped by the "
                          "cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearse the multi-rank path on one GPU: all ranks on device 0, gloo "
+                         "collectives on host tensors (tests only; not a scaling measurement)")
     ap.add_argument("--no-c1", action="store_true",
                     help="skip config C1's line (8k-point P2P pairs, CPU and GPU)")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
@@ -266,10 +272,16 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
+    # --share-gpu (a rehearsal of the N-rank path on a one-GPU box): every rank on device 0,
+    # collectives over gloo on host tensors; otherwise one GPU per rank and RCCL over xGMI
+    gpu = 0 if args.share_gpu else local
+    torch.cuda.set_device(gpu)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         group = dist.group.WORLD
 
     from lidar_slam_arvc_amd import _lib
@@ -277,12 +289,12 @@ def main():
 
     extra_ids = []                                   # (context, handle) of extra runs
     devs = [None]
-    dev = _lib.device(local)
+    dev = _lib.device(gpu)
     ids = [dev.upload(s) for s in seq.scans]        # raw scans resident in HBM
     want_normals = args.method == "p2plane"
     # pre-process normals mode: "lazy" computes only the target normals the registration reads
     wn_mode = ("lazy" if args.normals == "lazy" else True) if want_normals else False
-    cuda = torch.device("cuda", local)
+    cuda = torch.device("cpu") if args.share_gpu else torch.device("cuda", local)   # collectives
     ms = None
     if ouster:
         from lidar_slam_arvc_amd.multiscale import MultiScaleSet
@@ -314,26 +326,35 @@ def main():
         icp = _lib.icp_params(method=args.method)
         S = max(1, min(args.streams, P))
         cut = [round(k * P / S) for k in range(S + 1)]          # pair runs [cut[s], cut[s+1])
-        devs = [dev] + [_lib.Device(local) for _ in range(S - 1)]
+        devs = [dev] + [_lib.Device(gpu) for _ in range(S - 1)]
         # run s owns keyframes cut[s] .. cut[s+1] (the shared end keyframe is in both runs)
         run_ids = [ids[cut[0]:cut[1] + 1]] + [[devs[k].upload(seq.scans[j])
                                                 for j in range(cut[k], cut[k + 1] + 1)]
                                                for k in range(1, S)]
         extra_ids.extend((devs[k], h) for k in range(1, S) for h in run_ids[k])
 
-        def run(k, out):
+        def run(k, out, gates):
             d, hs = devs[k], run_ids[k]
-            n = d.preprocess(hs, prep)
+            if gates is not None and k > 0:
+                gates[k - 1].wait()     # --stagger: pre-process after the previous run's
+            try:
+                n = d.preprocess(hs, prep)
+            finally:
+                if gates is not None:
+                    gates[k].set()
             out[k] = (n if k == 0 else n[1:], d.icp_batch_arrays(hs[1:], hs[:-1],
                                                                  seq.priors[cut[k]:cut[k + 1]],
                                                                  icp))
 
         def step():
             out = [None] * S
-            th = [threading.Thread(target=run, args=(k, out)) for k in range(1, S)]
+            # --stagger: run k pre-processes (VALU-bound normals) while run k - 1 registers
+            # (latency-bound ICP passes) -- a pipeline over the sequence's chunks
+            gates = [threading.Event() for _ in range(S)] if args.stagger else None
+            th = [threading.Thread(target=run, args=(k, out, gates)) for k in range(1, S)]
             for t in th:
                 t.start()
-            run(0, out)
+            run(0, out, gates)
             for t in th:
                 t.join()
             if any(o is None for o in out):
