@@ -1685,6 +1685,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
         if (done) break;
         hipEvent_t ev;
+        // LSM_NN_XLDS=<bytes> (diagnostics, read per call): extra dynamic LDS per workgroup,
+        // lowering the correspondence kernel's occupancy (the occupancy-sensitivity probe)
+        const char *nxl = getenv("LSM_NN_XLDS");
+        const size_t nn_xlds = nxl ? size_t(atol(nxl)) : 0;
         ctx->tic("nn", &ev);
         if (d_nst) {
             unsigned long long *sp = d_nst + size_t(pass) * NN_NSTAT;
@@ -1697,11 +1701,13 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                     tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass,
                     lz.blkflag, sp);
         } else if (pass < CERT_FROM || nocert)
-            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q,
-                                                          d_qn + pass, qcap, d_sqn + pass, lz.blkflag);
+            nn_kernel<false><<<grid, NN_THREADS, nn_xlds, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt,
+                                                                d_cert, d_q, d_qn + pass, qcap,
+                                                                d_sqn + pass, lz.blkflag);
         else
-            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q,
-                                                         d_qn + pass, qcap, d_sqn + pass, lz.blkflag);
+            nn_kernel<true><<<grid, NN_THREADS, nn_xlds, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt,
+                                                               d_cert, d_q, d_qn + pass, qcap,
+                                                               d_sqn + pass, lz.blkflag);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
         {

@@ -663,7 +663,10 @@ __device__ __forceinline__ void scan_run_pred(const float4 *xyz, uint32_t a, uin
 //           row and add the `need` smallest by (d2, k).
 constexpr int NB8 = 128;          // level-0 bins (u8 counters)
 constexpr int NB32 = 32;          // refinement bins (u32 counters)
-constexpr int HSTRIDE = 33;       // LDS words per lane: 128 u8 / 32 u32 bins, padded to odd
+#ifndef LSM_HSTRIDE
+#define LSM_HSTRIDE 33
+#endif
+constexpr int HSTRIDE = LSM_HSTRIDE;   // LDS words per lane: 128 u8 / 32 u32 bins, padded to odd
 // members collected by the final pass: 2 words per entry (the f32 rounding of the exact f64 d2,
 // a monotone key, and the index; f32 ties are ordered by recomputing the exact f64 d2), so 16
 // fit a lane's row. A chosen bin holding more needs a refine scan: 1.1 % of the dense points
@@ -715,6 +718,19 @@ __device__ __forceinline__ void sel_thresholds(const Sel &S, const NormalParams 
     below32 = np.preclass && lo_t > 0.0 ? float(lo_t * (1.0 - 2e-6)) : -1.f;
     above32 = np.preclass && hi_t < 1e30 ? float(hi_t * (1.0 + 2e-6)) : INFINITY;
 }
+
+// A lane's LDS row. With HSTRIDE == 32 (no padding word: five 256-lane workgroups fit a CU's
+// 160 KB) word w is stored at w ^ (lane & 31), so the loops in which every lane touches the same
+// word of its own row (clearing, bin selection, member ranking) hit 32 distinct banks.
+struct HRow {
+    uint32_t *p;
+    uint32_t sw;
+    __device__ __forceinline__ uint32_t *at(uint32_t w) const { return p + (w ^ sw); }
+    __device__ __forceinline__ uint32_t &operator[](uint32_t w) const { return p[w ^ sw]; }
+    __device__ __forceinline__ uint32_t byte(uint32_t b) const {   // u8 bin b
+        return reinterpret_cast<const uint8_t *>(p)[((b >> 2) ^ sw) * 4 + (b & 3)];
+    }
+};
 
 // fire-and-forget LDS add (ds_add_u32: no read-back, so the walk does not wait on LDS)
 __device__ __forceinline__ void lds_add(uint32_t *a, uint32_t v) {
@@ -784,11 +800,11 @@ template <int G, typename Acc, bool PH = false>
 __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                             unsigned long long *stats, uint32_t *H, Acc &acc,
                             NPhase *ph = nullptr) {
-    uint8_t *H8 = reinterpret_cast<uint8_t *>(H);
+    const HRow R{H, HSTRIDE == 32 ? (__lane_id() & 31u) : 0u};
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
-#pragma unroll
-    for (int b = 0; b < NB8 / 4; ++b) H[b] = 0;
+#pragma unroll 1   // (unrolled, the 32 swizzled word addresses stay live across the scans)
+    for (int b = 0; b < NB8 / 4; ++b) R[b] = 0;
     Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
     bool sat = false;
     int count = 0;
@@ -818,7 +834,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                 NP_ST(ph, 1, 1u);
                 if (!dense) acc.add(p, k);
                 ++count;
-                lds_add(H + (bb >> 2), 1u << ((bb & 3) << 3));   // u8 bin, carries detected below
+                lds_add(R.at(bb >> 2), 1u << ((bb & 3) << 3));   // u8 bin, carries detected below
             }
         });
     });
@@ -839,9 +855,9 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         // such carry lowers the bin total by 255 or 256, so the total tells.
         if (count > 255) {
             uint32_t tot = 0;
-#pragma unroll
+#pragma unroll 1
             for (int b = 0; b < NB8 / 4; ++b) {
-                const uint32_t w = H[b];
+                const uint32_t w = R[b];
                 tot += (w & 0xffu) + ((w >> 8) & 0xffu) + ((w >> 16) & 0xffu) + (w >> 24);
             }
             sat = tot != uint32_t(count);
@@ -850,8 +866,8 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // rescan the members of the current state: their key extremes and a histogram by `next`
     auto refine = [&](const Sel &next, double &dmin, double &dmax, uint32_t &kmin, uint32_t &kmax) {
         NP_ST(ph, 6, 1u);
-#pragma unroll
-        for (int b = 0; b < NB32; ++b) H[b] = 0;
+#pragma unroll 1
+        for (int b = 0; b < NB32; ++b) R[b] = 0;
         dmin = INFINITY;
         dmax = -INFINITY;
         kmin = 0xffffffffu;
@@ -861,7 +877,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                 NP_ST(ph, 2, in ? 1u : 0u);
                 Off o;
                 if (in && in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
-                    lds_add(H + sel_level_bin(next, o.d2, k), 1u);
+                    lds_add(R.at(sel_level_bin(next, o.d2, k)), 1u);
                     dmin = fmin(dmin, o.d2);
                     dmax = fmax(dmax, o.d2);
                     kmin = min(kmin, k);
@@ -888,14 +904,14 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         uint32_t acc = 0;
         int bstar = S.nb - 1;
         for (int b = 0; b < S.nb; ++b) {
-            const uint32_t hb = u8 ? uint32_t(H8[b]) : H[b];
+            const uint32_t hb = u8 ? R.byte(b) : R[b];
             if (acc + hb >= need) {
                 bstar = b;
                 break;
             }
             acc += hb;
         }
-        const uint32_t bin_count = u8 ? uint32_t(H8[bstar]) : H[bstar];
+        const uint32_t bin_count = u8 ? R.byte(bstar) : R[bstar];
         need -= acc;
         S.b = bstar;
         if (!S.by_idx) top = fmin(top, S.lo + double(bstar + 1) / S.scale);
@@ -956,8 +972,8 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                 acc.add(p, k);
             } else if (cl == 0) {
                 if (m < SEL_CAP) {
-                    H[2 * m] = __float_as_uint(float(o.d2));
-                    H[2 * m + 1] = k;
+                    R[2 * m] = __float_as_uint(float(o.d2));
+                    R[2 * m + 1] = k;
                 }
                 ++m;
             }
@@ -965,18 +981,18 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     });
     const uint32_t mm = m < SEL_CAP ? m : SEL_CAP;
     for (uint32_t e = 0; e < mm; ++e) {
-        const uint32_t fe = H[2 * e];   // non-negative floats order like their bit patterns
-        const uint32_t ke = H[2 * e + 1];
+        const uint32_t fe = R[2 * e];   // non-negative floats order like their bit patterns
+        const uint32_t ke = R[2 * e + 1];
         uint32_t rank = 0;
         double de = -1.0;   // exact d2 of e, computed at its first f32 tie
         for (uint32_t g = 0; g < mm; ++g) {
-            const uint32_t fg = H[2 * g];
+            const uint32_t fg = R[2 * g];
             if (fg < fe) {
                 ++rank;
             } else if (fg == fe && g != e) {
                 // f32 keys tie: the exact (d2, index) order (the f32 rounding is monotone, so
                 // distinct keys already order like the exact distances)
-                const uint32_t kg = H[2 * g + 1];
+                const uint32_t kg = R[2 * g + 1];
                 if (de < 0.0) de = make_off(lsm_ld(C.xyz, ke), qx, qy, qz).d2;
                 const double dg = make_off(lsm_ld(C.xyz, kg), qx, qy, qz).d2;
                 rank += (dg < de || (dg == de && kg < ke)) ? 1u : 0u;
@@ -1021,8 +1037,13 @@ NormalParams normal_params(double radius, int max_nn) {
     return np;
 }
 
+#ifdef LSM_NORMALS_WPE
+#define LSM_NORMALS_ATTR __attribute__((amdgpu_waves_per_eu(LSM_NORMALS_WPE)))
+#else
+#define LSM_NORMALS_ATTR
+#endif
 template <int G>
-__global__ void __launch_bounds__(PT_THREADS)
+__global__ void __launch_bounds__(PT_THREADS) LSM_NORMALS_ATTR
 normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
                unsigned long long *stats) {
     __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
@@ -1797,10 +1818,14 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                     fprintf(stderr, "  %-13s %10.3f %10.3f\n", nm[c], double(h[c]) / double(npts),
                             double(h[8 + c]) * 64.0 / double(npts));
             }
-            if (G == 1) normals_kernel<1><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
-            else if (G == 2) normals_kernel<2><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
-            else if (G == 8) normals_kernel<8><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
-            else normals_kernel<4><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ns);
+            // LSM_NORMALS_XLDS=<bytes> (diagnostics, read per call): extra dynamic LDS per
+            // workgroup, lowering the kernel's occupancy (the occupancy-sensitivity probe)
+            const char *xl = getenv("LSM_NORMALS_XLDS");
+            const size_t xlds = xl ? size_t(atol(xl)) : 0;
+            if (G == 1) normals_kernel<1><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
+            else if (G == 2) normals_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
+            else if (G == 8) normals_kernel<8><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
+            else normals_kernel<4><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
             if (nstats) {
                 unsigned long long h[72] = {};
                 LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ns, sizeof(h), hipMemcpyDeviceToHost, st));
