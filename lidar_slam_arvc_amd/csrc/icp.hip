@@ -237,6 +237,59 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
     // rightwards from lo (x >= qx), then leftwards from lo - 1 (x < qx). LSM_NN_PF: the first
     // groups of both walks are loaded together, and each walk loads its next group before
     // testing the current one (loads clamped to the run).
+#if LSM_NN_PF == 2
+    // the same walks over two register buffers each (the next group loads into the buffer not
+    // being tested: no copies rotate the pipeline)
+    float4 ra[NN_G], rb[NN_G], la[NN_G], lb[NN_G];
+#pragma unroll
+    for (int g = 0; g < NN_G; ++g) {
+        ra[g] = lsm_ld(xyz, min(lo + uint32_t(g), b - 1));
+        la[g] = lsm_ld(xyz, uint32_t(max(int(lo) - 1 - g, int(a))));
+    }
+    auto right = [&](const float4 (&t)[NN_G], uint32_t k) {
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) {
+            const float dx = t[g].x - qx;
+            if (k + uint32_t(g) >= b || dx * dx + dyz2 > t2.lim) return false;
+            NN_ST(ns, 4, 1);
+            top_add(sqd(t[g], qx, qy, qz), int(k + uint32_t(g)), t2);
+        }
+        return true;
+    };
+    auto left = [&](const float4 (&t)[NN_G], int k) {
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) {
+            const float dx = qx - t[g].x;
+            if (k - g < int(a) || dx * dx + dyz2 > t2.lim) return false;
+            NN_ST(ns, 4, 1);
+            top_add(sqd(t[g], qx, qy, qz), k - g, t2);
+        }
+        return true;
+    };
+    for (uint32_t k = lo; k < b;) {
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) rb[g] = lsm_ld(xyz, min(k + uint32_t(NN_G + g), b - 1));
+        if (!right(ra, k)) break;
+        k += NN_G;
+        if (k >= b) break;
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) ra[g] = lsm_ld(xyz, min(k + uint32_t(NN_G + g), b - 1));
+        if (!right(rb, k)) break;
+        k += NN_G;
+    }
+    for (int k = int(lo) - 1; k >= int(a);) {
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) lb[g] = lsm_ld(xyz, uint32_t(max(k - NN_G - g, int(a))));
+        if (!left(la, k)) break;
+        k -= NN_G;
+        if (k < int(a)) break;
+#pragma unroll
+        for (int g = 0; g < NN_G; ++g) la[g] = lsm_ld(xyz, uint32_t(max(k - NN_G - g, int(a))));
+        if (!left(lb, k)) break;
+        k -= NN_G;
+    }
+    return;
+#endif
 #if LSM_NN_PF
     float4 r[NN_G], l[NN_G];
 #pragma unroll

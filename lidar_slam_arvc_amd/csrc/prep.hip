@@ -540,8 +540,17 @@ constexpr uint32_t SCAN_SLACK = 8;   // scan_run_pred: entry search stops within
 #define LSM_NORMALS_G_DEFAULT 2
 #endif
 constexpr int NORMALS_G_DEFAULT = LSM_NORMALS_G_DEFAULT;
+#ifndef LSM_NORMALS_GD_DEFAULT
+#define LSM_NORMALS_GD_DEFAULT 2
+#endif
+constexpr int NORMALS_GD_DEFAULT = LSM_NORMALS_GD_DEFAULT;
 #ifndef LSM_NORMALS_PF
 #define LSM_NORMALS_PF 1
+#endif
+// the dense half of the split launch (LDS-bound occupancy: registers to spare) may pipeline
+// over two register buffers (2)
+#ifndef LSM_NORMALS_PFD
+#define LSM_NORMALS_PFD LSM_NORMALS_PF
 #endif
 
 template <int G, typename Body>
@@ -588,19 +597,57 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
 // scan_run with the window test folded into a predicate: body(p, k, in) is called for every
 // loaded point until the walk passes xh, `in` telling whether it lies in the window (fewer
 // divergent branches per point than nested ifs).
-template <int G, typename Body>
-__device__ __forceinline__ void scan_run_pred(const float4 *xyz, uint32_t a, uint32_t b, float xl,
+// Point readers of the normals walks: plain global loads (64-bit addresses), or buffer loads
+// through a descriptor of the cloud's points (a 32-bit offset per load; the constant offsets of
+// a load group fold into the instructions), LSM_NORMALS_BUF.
+struct GlobalPts {
+    const float4 *xyz;
+    __device__ __forceinline__ float4 pt(uint32_t k) const { return lsm_ld(xyz, k); }
+    __device__ __forceinline__ float x(uint32_t k) const {
+        return lsm_ld(reinterpret_cast<const float *>(xyz), size_t(k) * 4);
+    }
+};
+struct BufPts {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ float4 pt(uint32_t k) const {
+        typedef float v4 __attribute__((ext_vector_type(4)));
+        const v4 v = __builtin_bit_cast(v4, __builtin_amdgcn_raw_buffer_load_b128(r, int(k * 16u), 0, 0));
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+    __device__ __forceinline__ float x(uint32_t k) const {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, int(k * 16u), 0, 0));
+    }
+};
+#ifndef LSM_NORMALS_BUF
+#define LSM_NORMALS_BUF 1
+#endif
+#if LSM_NORMALS_BUF
+typedef BufPts NormalsPts;
+// the descriptor of cloud C's points (C is wave-uniform in every normals kernel), its range
+// covering the LSM_XYZ_PAD spare points the prefetching walks may read
+__device__ __forceinline__ BufPts normals_pts(const CloudDev &C) {
+    return BufPts{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(C.xyz), 0,
+                                                    (C.n + LSM_XYZ_PAD) * 16, 0x00020000)};
+}
+#else
+typedef GlobalPts NormalsPts;
+__device__ __forceinline__ GlobalPts normals_pts(const CloudDev &C) { return GlobalPts{C.xyz}; }
+#endif
+
+// body(p, k, in): `in` is the walk's liveness only -- the points a window search leaves before
+// xl (at most SCAN_SLACK) lie outside the ball and fail the bodies' own exact tests, so the
+// window's left edge needs no test of its own.
+template <int G, int PF, typename Rd, typename Body>
+__device__ __forceinline__ void scan_run_pred(const Rd &xyz, uint32_t a, uint32_t b, float xl,
                                               float xh, Body &&body) {
     if (b - a > SCAN_BSEARCH) {
         // 4-ary search (three probes per round trip) for a start at most SCAN_SLACK points
         // before the window's first point: the walk skips x < xl anyway
         uint32_t lo = a, hi = b;   // the first x >= xl lies in [lo, hi]
-        const float *xs = reinterpret_cast<const float *>(xyz);
         while (hi - lo > SCAN_SLACK) {
             const uint32_t q = (hi - lo) >> 2;
             const uint32_t m1 = lo + q, m2 = lo + 2 * q, m3 = lo + 3 * q;
-            const float x1 = lsm_ld(xs, size_t(m1) * 4), x2 = lsm_ld(xs, size_t(m2) * 4),
-                        x3 = lsm_ld(xs, size_t(m3) * 4);
+            const float x1 = xyz.x(m1), x2 = xyz.x(m2), x3 = xyz.x(m3);
             if (x3 < xl) lo = m3 + 1;
             else if (x2 < xl) { lo = m2 + 1; hi = m3; }
             else if (x1 < xl) { lo = m1 + 1; hi = m2; }
@@ -608,6 +655,37 @@ __device__ __forceinline__ void scan_run_pred(const float4 *xyz, uint32_t a, uin
         }
         a = lo;
     }
+if constexpr (PF == 2) {
+    // software-pipelined over two register buffers (the next group loads into the buffer not
+    // being tested, so no copies rotate the pipeline); loads may run up to 2G - 1 points past
+    // the run: within the cloud's LSM_XYZ_PAD spare points
+    static_assert(2 * G - 1 <= LSM_XYZ_PAD, "prefetched group loads run past a run");
+    if (a >= b) return;
+    float4 pa[G], pb[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) pa[g] = xyz.pt(a + uint32_t(g));
+    auto test = [&](const float4 (&p)[G], uint32_t k) {
+        bool live = true;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            live = live && (k + uint32_t(g) < b) && !(p[g].x > xh);
+            body(p[g], k + uint32_t(g), live);
+        }
+        return live;
+    };
+    for (uint32_t k = a;;) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) pb[g] = xyz.pt(k + uint32_t(G + g));
+        if (!test(pa, k)) break;
+        k += G;
+        if (k >= b) break;
+#pragma unroll
+        for (int g = 0; g < G; ++g) pa[g] = xyz.pt(k + uint32_t(G + g));
+        if (!test(pb, k)) break;
+        k += G;
+        if (k >= b) break;
+    }
+    } else {
 #if LSM_NORMALS_PF
     // software-pipelined: the next group's loads are in flight while this group is tested (the
     // loads may run up to 2G - 1 points past the run: within the cloud's LSM_XYZ_PAD spare points)
@@ -615,28 +693,29 @@ __device__ __forceinline__ void scan_run_pred(const float4 *xyz, uint32_t a, uin
     if (a >= b) return;
     float4 nx[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) nx[g] = lsm_ld(xyz, a + uint32_t(g));
+    for (int g = 0; g < G; ++g) nx[g] = xyz.pt(a + uint32_t(g));
     for (uint32_t k = a; k < b; k += G) {
         float4 p[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             p[g] = nx[g];
-            nx[g] = lsm_ld(xyz, k + uint32_t(G + g));
+            nx[g] = xyz.pt(k + uint32_t(G + g));
         }
 #else
     static_assert(G <= LSM_XYZ_PAD, "group loads may run LSM_XYZ_PAD points past a run");
     for (uint32_t k = a; k < b; k += G) {
         float4 p[G];
 #pragma unroll
-        for (int g = 0; g < G; ++g) p[g] = lsm_ld(xyz, k + uint32_t(g));
+        for (int g = 0; g < G; ++g) p[g] = xyz.pt(k + uint32_t(g));
 #endif
         bool live = true;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             live = live && (k + uint32_t(g) < b) && !(p[g].x > xh);
-            body(p[g], k + uint32_t(g), live && p[g].x >= xl);
+            body(p[g], k + uint32_t(g), live);
         }
         if (!live) break;
+    }
     }
 }
 
@@ -749,7 +828,9 @@ struct CumAcc {
     const float4 *prior;
     __device__ void add(const float4 &p, uint32_t) { cum_add_pt(c, p, qx, qy, qz); }
     __device__ void reset() { c = Cum{}; }
-    __device__ void finish() { *out = normal_from_cum(c, prior); }
+    __device__ void finish() {
+        if (out) *out = normal_from_cum(c, prior);   // (out null: a lane without a point)
+    }
 };
 
 // ListAcc: the neighbour indices (sorted order) and exact f64 squared distances, unordered.
@@ -796,34 +877,162 @@ struct NPhase {
         if (PH) (ph)->v[c] += (x);   \
     } while (0)
 
-template <int G, typename Acc, bool PH = false>
-__device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
+// hybrid_lane modes. NL_AUTO: the whole procedure. The split launch (normals_sparse_kernel +
+// normals_dense_kernel) runs it in two halves with the same decisions and the same summation
+// order, so every normal is bit-identical to NL_AUTO's:
+//   NL_SPARSE: a point predicted dense is deferred at once; otherwise scan 1 (cumulants and
+//              count, no histogram: no LDS) finishes it when count <= max_nn, else defers it;
+//   NL_DENSE:  a deferred point, as NL_AUTO runs a predicted-dense one (scan 1 builds the
+//              histogram only; a point with count <= max_nn then takes the final pass whole,
+//              which adds its ball in scan 1's order -- NL_AUTO's sums for either prediction).
+//   NL_COOP:   NL_DENSE with scan 1 and the final pass run cooperatively by the wave
+//              (coop_visit); every lane of the wave must call it (`act` false: no point).
+// Returns false when the point was deferred.
+constexpr int NL_AUTO = 0, NL_SPARSE = 1, NL_DENSE = 2, NL_COOP = 3;
+
+// wave-uniform min / max (readfirstlane: the result is known uniform, an SGPR value)
+__device__ __forceinline__ int wave_uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float wave_minf(float v) {
+    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, LSM_WAVE));
+    return __int_as_float(wave_uni(__float_as_int(v)));
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, LSM_WAVE));
+    return __int_as_float(wave_uni(__float_as_int(v)));
+}
+__device__ __forceinline__ int wave_mini(int v) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, LSM_WAVE));
+    return wave_uni(v);
+}
+__device__ __forceinline__ int wave_maxi(int v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, LSM_WAVE));
+    return wave_uni(v);
+}
+__device__ __forceinline__ float lane_f(float v, int i) {   // lane i's v (i wave-uniform)
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+}
+
+// Cooperative visit of the balls of a wave's 64 points (radius rad per lane; lanes with !act
+// take no part): the rows of the union of their ball boxes in ball_visit_runs' order (z, then
+// y, then the row's block parts left to right), each row's runs loaded 64 points at a time
+// (one coalesced load per chunk) and cut to the union of the lanes' x windows by two ballots
+// (the runs are x-sorted). Every lane tests every candidate of the chunk, broadcast from its
+// lane in order: cls(p, k) classifies it for this lane (and returns true when the point is to be
+// added); the lane's adds of the chunk then run in order, add(p, k), in a loop of the wave's
+// maximum add count in which every lane takes part in the broadcast. A lane thus sees its ball
+// points in exactly the order of its own ball_visit_runs walk -- the same classifications, the
+// same cumulant sums -- from candidates it does not have to chase one memory round trip at a
+// time. Points outside a lane's ball are rejected by its own exact tests (the per-lane windows
+// were only a pruning device).
+template <typename Cls, typename Add>
+__device__ __forceinline__ void coop_visit(const CloudDev &C, float4 qf, float rad, bool act,
+                                           Cls &&cls, Add &&add) {
+    int ylo, yhi, zlo, zhi;
+    axis_range(qf.y, C.oy, C.inv_cell, rad, C.ny, ylo, yhi);
+    axis_range(qf.z, C.oz, C.inv_cell, rad, C.nz, zlo, zhi);
+    if (!act) {
+        ylo = zlo = 0x7fffffff;
+        yhi = zhi = -1;
+    }
+    const int Zlo = wave_mini(zlo), Zhi = wave_maxi(zhi);
+    const int Ylo = wave_mini(ylo), Yhi = wave_maxi(yhi);
+    const float prune = rad * 1.0001f + 1e-6f;
+    const float prune2 = prune * prune;
+    const int lane = __lane_id();
+#pragma unroll 1
+    for (int z = Zlo; z <= Zhi; ++z) {
+        const float dz2 = slab_d2(qf.z, C.oz, C.cell, z);
+#pragma unroll 1
+        for (int y = Ylo; y <= Yhi; ++y) {
+            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
+            const bool need = act && z >= zlo && z <= zhi && y >= ylo && y <= yhi && !(dyz2 > prune2);
+            if (__ballot(need) == 0) continue;
+            float xl = INFINITY, xh = -INFINITY;
+            if (need) {   // the row's chord window, as ball_visit_runs widens it
+                const float ch = sqrtf(prune2 - dyz2) * 1.0001f + 1e-6f * fabsf(qf.x) + 1e-5f;
+                xl = qf.x - ch;
+                xh = qf.x + ch;
+            }
+            const float XL = wave_minf(xl), XH = wave_maxf(xh);
+            // the cells of x in [XL, XH] (slack for the f32 cell coordinates, as axis_range)
+            const int xa = max((int)floorf((XL - C.ox) * C.inv_cell - 1e-3f), 0);
+            const int xb = min((int)floorf((XH - C.ox) * C.inv_cell + 1e-3f), C.nx - 1);
+            int x = xa;
+#pragma unroll 1
+            while (x <= xb) {
+                const int xe = wave_uni(min(xb, x | (LSM_BLK - 1)));
+                const uint32_t a = lsm_ld(C.cell_start, lsm_cell_lin(C.nbx, C.nby, x, y, z));
+                const uint32_t b = lsm_ld(C.cell_start, lsm_cell_lin(C.nbx, C.nby, xe, y, z) + 1);
+                x = xe + 1;
+#pragma unroll 1
+                for (uint32_t pos = a; pos < b; pos += LSM_WAVE) {
+                    const uint32_t cnt = min(uint32_t(LSM_WAVE), b - pos);
+                    const float4 c = lsm_ld(C.xyz, pos + min(uint32_t(lane), cnt - 1));
+                    const bool valid = uint32_t(lane) < cnt;
+                    const int i0 = __popcll(__ballot(valid && c.x < XL));
+                    const int i1 = __popcll(__ballot(valid && !(c.x > XH)));
+                    uint64_t addm = 0;
+#pragma unroll 2
+                    for (int i = i0; i < i1; ++i) {
+                        const float4 p = make_float4(lane_f(c.x, i), lane_f(c.y, i), lane_f(c.z, i), 0.f);
+                        if (act && cls(p, pos + uint32_t(i))) addm |= uint64_t(1) << i;
+                    }
+                    const int rounds = wave_maxi(__popcll(addm));
+#pragma unroll 1
+                    for (int r = 0; r < rounds; ++r) {
+                        const bool has = addm != 0;
+                        const int i = has ? __ffsll((unsigned long long)addm) - 1 : 0;
+                        addm &= addm - 1;
+                        const float px = __shfl(c.x, i, LSM_WAVE), py = __shfl(c.y, i, LSM_WAVE),
+                                    pz = __shfl(c.z, i, LSM_WAVE);
+                        if (has) add(make_float4(px, py, pz, 0.f), pos + uint32_t(i));
+                    }
+                    if (i1 < int(cnt)) break;   // the rest of the run lies past every window
+                }
+            }
+        }
+    }
+}
+
+template <int G, typename Acc, bool PH = false, int MODE = NL_AUTO, int PF = LSM_NORMALS_PF>
+__device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                             unsigned long long *stats, uint32_t *H, Acc &acc,
-                            NPhase *ph = nullptr) {
+                            NPhase *ph = nullptr, bool act = true) {
     const HRow R{H, HSTRIDE == 32 ? (__lane_id() & 31u) : 0u};
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
+    const NormalsPts pts = normals_pts(C);
+    // Dense-predicted points skip acc.add in scan 1 (histogram only); a wrong guess costs one
+    // plain rescan below, which visits the ball in scan 1's order (identical sums).
+    const bool dense = (MODE == NL_DENSE || MODE == NL_COOP) ? true : predict_dense(C, np, qf);
+    if (MODE == NL_SPARSE && dense) return false;
+    NP_ST(ph, 7, dense ? 1u : 0u);
+    if (MODE != NL_SPARSE) {
 #pragma unroll 1   // (unrolled, the 32 swizzled word addresses stay live across the scans)
-    for (int b = 0; b < NB8 / 4; ++b) R[b] = 0;
+        for (int b = 0; b < NB8 / 4; ++b) R[b] = 0;
+    }
     Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
     bool sat = false;
     int count = 0;
-    // Dense-predicted points skip acc.add in scan 1 (histogram only); a wrong guess costs one
-    // plain rescan below, which visits the ball in scan 1's order (identical sums).
-    const bool dense = predict_dense(C, np, qf);
-    NP_ST(ph, 7, dense ? 1u : 0u);
     // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
     // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
     // f32 d^2 and the scale are within 4.2e-7 relative, t < 128). The rest (the sphere's
     // rounding band, bin edges) take the exact f64 distance, so the histogram is the one the
     // f64 binning of the later scans implies.
-    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+    auto scan1 = [&](const float4 &p, uint32_t k, bool in) {
             NP_ST(ph, 0, in ? 1u : 0u);
             const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
             const float f = dx * dx + dy * dy + dz * dz;
+            if (MODE == NL_SPARSE) {   // the same ball membership as the binned test below
+                if (in && (f < np.r2_lo ||
+                           (f <= np.r2_hi && make_off(p, qx, qy, qz).d2 < np.r2))) {
+                    acc.add(p, k);
+                    ++count;
+                }
+                return;
+            }
             const float t = f * np.hscale;
-            const float fr = t - floorf(t);
+            const float fr = __builtin_amdgcn_fractf(t);   // t - floor(t) (v_fract)
             const bool fast = in && f < np.r2_lo && fr > 2e-4f && fr < 1.f - 2e-4f;
             int bb = fast ? int(t) : -1;
             if (in && !fast && f <= np.r2_hi) {   // the sphere's rounding band, bin edges
@@ -836,14 +1045,28 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                 ++count;
                 lds_add(R.at(bb >> 2), 1u << ((bb & 3) << 3));   // u8 bin, carries detected below
             }
+    };
+    if (MODE == NL_COOP) {
+        coop_visit(C, qf, np.r, act, [&](const float4 &p, uint32_t k) {
+            scan1(p, k, true);
+            return false;
+        }, [](const float4 &, uint32_t) {});
+    } else {
+        ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+            scan_run_pred<G, PF>(pts, a, b, xl, xh, scan1);
         });
-    });
+    }
+    if (MODE == NL_SPARSE) {
+        if (count > np.max_nn) return false;
+        acc.finish();
+        return true;
+    }
     double top = np.r2;   // every point below or member has d2 <= top (up to rounding)
     uint32_t need = uint32_t(np.max_nn);   // still to take from the members
     if (count <= np.max_nn) {
         if (!dense) {
             acc.finish();
-            return;
+            return true;
         }
         S.dlo = INFINITY;   // mispredicted: every ball point is below, the final pass adds them
         need = 0;
@@ -873,7 +1096,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         kmin = 0xffffffffu;
         kmax = 0u;
         ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
-            scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+            scan_run_pred<G, PF>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
                 NP_ST(ph, 2, in ? 1u : 0u);
                 Off o;
                 if (in && in_ball(np, qf, qx, qy, qz, p, o) && sel_classify(S, o.d2, k) == 0) {
@@ -954,31 +1177,42 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     float below32, above32;
     sel_thresholds(S, np, below32, above32);
     uint32_t m = 0;
-    ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run_pred<G>(C.xyz, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
-            NP_ST(ph, 3, in ? 1u : 0u);
-            const float fd = f32_d2(qf, p);
-            if (!in || fd > np.r2_hi || fd > above32) return;
-            if (fd < below32) {
-                NP_ST(ph, 4, 1u);
-                acc.add(p, k);
-                return;
+    // final-pass classification of one point: true = add it now (below); members are collected
+    auto fin = [&](const float4 &p, uint32_t k, bool in) -> bool {
+        NP_ST(ph, 3, in ? 1u : 0u);
+        const float fd = f32_d2(qf, p);
+        if (!in || fd > np.r2_hi || fd > above32) return false;
+        if (fd < below32) {
+            NP_ST(ph, 4, 1u);
+            return true;
+        }
+        const Off o = make_off(p, qx, qy, qz);
+        if (fd >= np.r2_lo && !(o.d2 < np.r2)) return false;
+        const int cl = sel_classify(S, o.d2, k);
+        if (cl < 0) {
+            NP_ST(ph, 4, 1u);
+            return true;
+        }
+        if (cl == 0) {
+            if (m < SEL_CAP) {
+                R[2 * m] = __float_as_uint(float(o.d2));
+                R[2 * m + 1] = k;
             }
-            const Off o = make_off(p, qx, qy, qz);
-            if (fd >= np.r2_lo && !(o.d2 < np.r2)) return;
-            const int cl = sel_classify(S, o.d2, k);
-            if (cl < 0) {
-                NP_ST(ph, 4, 1u);
-                acc.add(p, k);
-            } else if (cl == 0) {
-                if (m < SEL_CAP) {
-                    R[2 * m] = __float_as_uint(float(o.d2));
-                    R[2 * m + 1] = k;
-                }
-                ++m;
-            }
+            ++m;
+        }
+        return false;
+    };
+    if (MODE == NL_COOP) {
+        coop_visit(C, qf, sel_radius(top, np.r), act,
+                   [&](const float4 &p, uint32_t k) { return fin(p, k, true); },
+                   [&](const float4 &p, uint32_t k) { acc.add(p, k); });
+    } else {
+        ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
+            scan_run_pred<G, PF>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+                if (fin(p, k, in)) acc.add(p, k);
+            });
         });
-    });
+    }
     const uint32_t mm = m < SEL_CAP ? m : SEL_CAP;
     for (uint32_t e = 0; e < mm; ++e) {
         const uint32_t fe = R[2 * e];   // non-negative floats order like their bit patterns
@@ -1001,6 +1235,7 @@ __device__ void hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         if (rank < need) acc.add(lsm_ld(C.xyz, ke), ke);
     }
     acc.finish();
+    return true;
 }
 
 // Own-cell population from which a point is predicted to have more than max_nn neighbours in
@@ -1059,6 +1294,87 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     // algorithmic work of the normals (9 cumulant FMAs per neighbour), summed
     // over 64 counters to spread the atomics
     if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+}
+
+// Split launch, first half: the points predicted sparse (NL_SPARSE, no LDS). Deferred points are
+// appended to their cloud's dense list dlist[geo.pt_off + ...] (wave-aggregated; the order of
+// the list does not matter: every point's computation is independent of the others).
+#ifdef LSM_NSPARSE_WPE
+#define LSM_NSPARSE_ATTR __attribute__((amdgpu_waves_per_eu(LSM_NSPARSE_WPE)))
+#else
+#define LSM_NSPARSE_ATTR
+#endif
+template <int G>
+__global__ void __launch_bounds__(PT_THREADS) LSM_NSPARSE_ATTR
+normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
+                      uint32_t *dlist, uint32_t *dcnt, unsigned long long *stats) {
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int j = s.start + threadIdx.x;
+    bool defer = false;
+    if (j < C.n) {
+        const float4 q = lsm_ld(C.xyz, j);
+        CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
+                   C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
+        defer = !hybrid_lane<G, CumAcc, false, NL_SPARSE>(C, j, np, nullptr, nullptr, acc);
+        if (stats && !defer) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+    }
+    const uint64_t bm = __ballot(defer);
+    if (bm) {
+        const int lane = threadIdx.x & 63;
+        const int leader = __ffsll((unsigned long long)bm) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(dcnt + s.cloud, uint32_t(__popcll(bm)));
+        base = __shfl(base, leader, LSM_WAVE);
+        if (defer)
+            dlist[geo[s.cloud].pt_off + base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = uint32_t(j);
+    }
+}
+
+// Split launch, second half: one lane per entry of the clouds' dense lists (NL_DENSE), so the
+// truncated neighbourhoods run in full waves. The grid is the first half's (a cloud's list never
+// holds more entries than the cloud has points); workgroups past the list return at once.
+template <int G>
+__global__ void __launch_bounds__(PT_THREADS) LSM_NORMALS_ATTR
+normals_dense_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
+                     const uint32_t *dlist, const uint32_t *dcnt, unsigned long long *stats) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    const Seg s = segs[blockIdx.x];
+    const uint32_t slot = uint32_t(s.start) + threadIdx.x;
+    if (slot >= dcnt[s.cloud]) return;
+    const CloudDev C = cd[s.cloud];
+    const int j = int(dlist[geo[s.cloud].pt_off + slot]);
+    const float4 q = lsm_ld(C.xyz, j);
+    CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
+               C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
+    hybrid_lane<G, CumAcc, false, NL_DENSE, LSM_NORMALS_PFD>(C, j, np, stats,
+                                                             lds + threadIdx.x * HSTRIDE, acc);
+    if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+}
+
+// normals_dense_kernel with the scans run cooperatively by each wave (NL_COOP, coop_visit):
+// lanes past the list end ride along without a point (they shadow the wave's first entry and
+// write nothing). LSM_NORMALS_COOP=0 selects the per-lane walks.
+template <int G>
+__global__ void __launch_bounds__(PT_THREADS) LSM_NORMALS_ATTR
+normals_dense_coop_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
+                          const uint32_t *dlist, const uint32_t *dcnt, unsigned long long *stats) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    const Seg s = segs[blockIdx.x];
+    const uint32_t n = dcnt[s.cloud];
+    const uint32_t slot = uint32_t(s.start) + threadIdx.x;
+    const uint32_t first = uint32_t(s.start) + (threadIdx.x & ~uint32_t(LSM_WAVE - 1));
+    if (first >= n) return;   // the whole wave is past the list
+    const bool act = slot < n;
+    const CloudDev C = cd[s.cloud];
+    const int j = int(dlist[geo[s.cloud].pt_off + (act ? slot : first)]);
+    const float4 q = lsm_ld(C.xyz, j);
+    CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z),
+               act ? const_cast<float4 *>(C.nrm) + j : nullptr,
+               C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
+    hybrid_lane<G, CumAcc, false, NL_COOP>(C, j, np, act ? stats : nullptr,
+                                           lds + threadIdx.x * HSTRIDE, acc, nullptr, act);
+    if (stats && act) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
 }
 
 // normals_kernel with phase statistics (LSM_NORMALS_PHASES=1, diagnostics): per counter the
@@ -1822,7 +2138,37 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
             // workgroup, lowering the kernel's occupancy (the occupancy-sensitivity probe)
             const char *xl = getenv("LSM_NORMALS_XLDS");
             const size_t xlds = xl ? size_t(atol(xl)) : 0;
-            if (G == 1) normals_kernel<1><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
+            // LSM_NORMALS_SPLIT (read per call; default on): the two-kernel launch
+            const char *sp = getenv("LSM_NORMALS_SPLIT");
+            const bool split = !sp || atoi(sp) != 0;
+            if (split) {
+                uint32_t *dlist = (uint32_t *)ctx->buf("n_dlist", N * 4);
+                uint32_t *dcnt = (uint32_t *)ctx->buf("n_dcnt", size_t(K) * 4);
+                if (!dlist || !dcnt) return LSM_ENOMEM;
+                LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, size_t(K) * 4, st));
+                // LSM_NORMALS_GD: points per load group of the dense half (its occupancy is
+                // set by the LDS rows, so it has registers to spare for wider groups)
+                static const int GD = [] {
+                    const char *e = getenv("LSM_NORMALS_GD");
+                    return e ? atoi(e) : NORMALS_GD_DEFAULT;
+                }();
+                if (G == 4)
+                    normals_sparse_kernel<4><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                else
+                    normals_sparse_kernel<2><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                const char *co = getenv("LSM_NORMALS_COOP");   // read per call
+                const bool coop = co && atoi(co) != 0;
+                if (coop)
+                    normals_dense_coop_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                else if (GD == 8)
+                    normals_dense_kernel<8><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                else if (GD == 4)
+                    normals_dense_kernel<4><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                else if (GD == 3)
+                    normals_dense_kernel<3><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                else
+                    normals_dense_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+            } else if (G == 1) normals_kernel<1><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
             else if (G == 2) normals_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
             else if (G == 8) normals_kernel<8><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
             else normals_kernel<4><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);

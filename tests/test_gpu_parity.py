@@ -126,6 +126,42 @@ def test_normals_preclassification_bit_identical(dev, seq64k, max_nn, monkeypatc
         _release(dev, ids)
 
 
+@pytest.mark.parametrize("max_nn", [300, 30])
+def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
+    """The split launch (default: the points predicted sparse, then every deferred point in
+    full waves of the clouds' dense lists; its dense half with per-lane walks or with the
+    wave-cooperative scans, LSM_NORMALS_COOP) against the one-kernel launch (LSM_NORMALS_SPLIT=0):
+    bit-identical normals on bench scans, under heavier truncation, on degenerate neighbourhoods
+    (duplicates saturating a u8 bin, a dense patch) and on clouds that carry prior normals
+    (EstimateNormals re-run on a cloud with normals orients to them)."""
+    rng = np.random.default_rng(11)
+    patch = np.c_[5.0 + rng.uniform(-0.2, 0.2, 1500), rng.uniform(-0.2, 0.2, 1500),
+                  0.002 * rng.standard_normal(1500)]
+    dup = np.repeat([[5.05, 0.03, 0.0]], 400, axis=0)
+    clouds = list(seq64k.scans[:3]) + [np.r_[patch, dup].astype(np.float32)]
+    prm = _lib.prep_params(max_nn=max_nn)
+    keep = _lib.prep_params(max_nn=max_nn, min_radius=-np.inf, max_radius=1e15,
+                            min_height=-1e15, max_height=1e15)
+    out = {}
+    for split, coop in (("1", "0"), ("1", "1"), ("0", "0")):
+        monkeypatch.setenv("LSM_NORMALS_SPLIT", split)
+        monkeypatch.setenv("LSM_NORMALS_COOP", coop)
+        ids = [dev.upload(c) for c in clouds]
+        try:
+            dev.preprocess(ids, prm)
+            first = [dev.download(i, normals=True)[1] for i in ids]
+            dev.preprocess(ids, keep)          # again, now with prior normals
+            second = [dev.download(i, normals=True)[1] for i in ids]
+            out[split + coop] = first + second
+        finally:
+            _release(dev, ids)
+    monkeypatch.delenv("LSM_NORMALS_SPLIT")
+    monkeypatch.delenv("LSM_NORMALS_COOP")
+    for variant in ("10", "11"):
+        for a, b in zip(out[variant], out["00"]):
+            assert np.array_equal(a, b), variant
+
+
 def test_normals_degenerate_neighbourhoods(dev):
     """kNN-300 truncation on pathological neighbourhoods: 400 exact duplicates of one point (one
     d2 value holds more than a u8 histogram bin can count and more than the selection buffer
