@@ -209,8 +209,13 @@ constexpr int NN_G = LSM_NN_G;
 #ifndef LSM_NN_PF
 #define LSM_NN_PF 1
 #endif
+// LSM_NN_BUF: the box walks read the target through a buffer descriptor (32-bit offsets)
+#ifndef LSM_NN_BUF
+#define LSM_NN_BUF 1
+#endif
 
-__device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t b, float qx,
+template <typename Rd>
+__device__ __forceinline__ void scan_run(const Rd &xyz, uint32_t a, uint32_t b, float qx,
                                          float qy, float qz, float dyz2, Top3 &t2, uint32_t lin,
                                          NNStat *ns = nullptr) {
     NN_ST(ns, 2, 1);
@@ -219,19 +224,18 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
         for (uint32_t k = a; k < b; k += NN_G) {
             float4 t[NN_G];
 #pragma unroll
-            for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, min(k + uint32_t(g), b - 1));
+            for (int g = 0; g < NN_G; ++g) t[g] = xyz.pt(min(k + uint32_t(g), b - 1));
 #pragma unroll
             for (int g = 0; g < NN_G; ++g)
                 if (k + uint32_t(g) < b) top_add(sqd(t[g], qx, qy, qz), int(k + uint32_t(g)), t2);
         }
         return;
     }
-    const float *xs = reinterpret_cast<const float *>(xyz);
     uint32_t lo = a, hi = b;
     while (lo < hi) {
         NN_ST(ns, 3, 1);
         const uint32_t mid = (lo + hi) >> 1;
-        if (lsm_ld(xs, size_t(mid) * 4) < qx) lo = mid + 1;
+        if (xyz.x(mid) < qx) lo = mid + 1;
         else hi = mid;
     }
     // rightwards from lo (x >= qx), then leftwards from lo - 1 (x < qx). LSM_NN_PF: the first
@@ -243,8 +247,8 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
     float4 ra[NN_G], rb[NN_G], la[NN_G], lb[NN_G];
 #pragma unroll
     for (int g = 0; g < NN_G; ++g) {
-        ra[g] = lsm_ld(xyz, min(lo + uint32_t(g), b - 1));
-        la[g] = lsm_ld(xyz, uint32_t(max(int(lo) - 1 - g, int(a))));
+        ra[g] = xyz.pt(min(lo + uint32_t(g), b - 1));
+        la[g] = xyz.pt(uint32_t(max(int(lo) - 1 - g, int(a))));
     }
     auto right = [&](const float4 (&t)[NN_G], uint32_t k) {
 #pragma unroll
@@ -268,23 +272,23 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
     };
     for (uint32_t k = lo; k < b;) {
 #pragma unroll
-        for (int g = 0; g < NN_G; ++g) rb[g] = lsm_ld(xyz, min(k + uint32_t(NN_G + g), b - 1));
+        for (int g = 0; g < NN_G; ++g) rb[g] = xyz.pt(min(k + uint32_t(NN_G + g), b - 1));
         if (!right(ra, k)) break;
         k += NN_G;
         if (k >= b) break;
 #pragma unroll
-        for (int g = 0; g < NN_G; ++g) ra[g] = lsm_ld(xyz, min(k + uint32_t(NN_G + g), b - 1));
+        for (int g = 0; g < NN_G; ++g) ra[g] = xyz.pt(min(k + uint32_t(NN_G + g), b - 1));
         if (!right(rb, k)) break;
         k += NN_G;
     }
     for (int k = int(lo) - 1; k >= int(a);) {
 #pragma unroll
-        for (int g = 0; g < NN_G; ++g) lb[g] = lsm_ld(xyz, uint32_t(max(k - NN_G - g, int(a))));
+        for (int g = 0; g < NN_G; ++g) lb[g] = xyz.pt(uint32_t(max(k - NN_G - g, int(a))));
         if (!left(la, k)) break;
         k -= NN_G;
         if (k < int(a)) break;
 #pragma unroll
-        for (int g = 0; g < NN_G; ++g) la[g] = lsm_ld(xyz, uint32_t(max(k - NN_G - g, int(a))));
+        for (int g = 0; g < NN_G; ++g) la[g] = xyz.pt(uint32_t(max(k - NN_G - g, int(a))));
         if (!left(lb, k)) break;
         k -= NN_G;
     }
@@ -294,8 +298,8 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
     float4 r[NN_G], l[NN_G];
 #pragma unroll
     for (int g = 0; g < NN_G; ++g) {
-        r[g] = lsm_ld(xyz, min(lo + uint32_t(g), b - 1));
-        l[g] = lsm_ld(xyz, uint32_t(max(int(lo) - 1 - g, int(a))));
+        r[g] = xyz.pt(min(lo + uint32_t(g), b - 1));
+        l[g] = xyz.pt(uint32_t(max(int(lo) - 1 - g, int(a))));
     }
 #endif
     for (uint32_t k = lo; k < b; k += NN_G) {
@@ -304,11 +308,11 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
 #pragma unroll
         for (int g = 0; g < NN_G; ++g) {
             t[g] = r[g];
-            r[g] = lsm_ld(xyz, min(k + uint32_t(NN_G + g), b - 1));
+            r[g] = xyz.pt(min(k + uint32_t(NN_G + g), b - 1));
         }
 #else
 #pragma unroll
-        for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, min(k + uint32_t(g), b - 1));
+        for (int g = 0; g < NN_G; ++g) t[g] = xyz.pt(min(k + uint32_t(g), b - 1));
 #endif
         bool stop = false;
 #pragma unroll
@@ -331,11 +335,11 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
 #pragma unroll
         for (int g = 0; g < NN_G; ++g) {
             t[g] = l[g];
-            l[g] = lsm_ld(xyz, uint32_t(max(k - NN_G - g, int(a))));
+            l[g] = xyz.pt(uint32_t(max(k - NN_G - g, int(a))));
         }
 #else
 #pragma unroll
-        for (int g = 0; g < NN_G; ++g) t[g] = lsm_ld(xyz, uint32_t(max(k - g, int(a))));
+        for (int g = 0; g < NN_G; ++g) t[g] = xyz.pt(uint32_t(max(k - g, int(a))));
 #endif
         bool stop = false;
 #pragma unroll
@@ -575,6 +579,11 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     const int z0 = max(cz - K, 0), z1 = min(cz + K, G.nz - 1);
     const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
     const uint32_t *cs = G.cell_start;
+#if LSM_NN_BUF
+    const BufPts gp = cloud_buf_pts(G);
+#else
+    const GlobalPts gp{G.xyz};
+#endif
     const int W = 2 * K + 1;
     // Rows are visited centre-out (offsets 0, -1, 1, -2, 2, ...: |offset| never decreases) and
     // a row at offset d in z (or y) is at least (|d| - 1) cells from the query's slab. Once that
@@ -616,7 +625,7 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
                 const int xe = min(xb, x | (LSM_BLK - 1));   // end of this block's row part
                 const uint32_t a = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, x, y, z));
                 const uint32_t b = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, xe, y, z) + 1);
-                if (b > a) scan_run(G.xyz, a, b, qx, qy, qz, wyz, t2, prm.lin, ns);
+                if (b > a) scan_run(gp, a, b, qx, qy, qz, wyz, t2, prm.lin, ns);
                 x = xe + 1;
             }
         }
@@ -754,8 +763,14 @@ __device__ __forceinline__ void flush_stats(const NNStat &ls, unsigned long long
     }
 }
 
-// LSM_NN_WPE=<w>: cap the correspondence kernel's registers for w waves per SIMD (A/B builds)
-#ifdef LSM_NN_WPE
+// LSM_NN_WPE=<w>: cap the correspondence kernel's registers for w waves per SIMD. 8 (64 VGPRs,
+// 2-4 registers spilled outside the walks) since the walks read the target through a buffer
+// descriptor: nn 81.7 -> 73.9 ms per step (7 waves: 76.1; round 2, with 64-bit addresses, the
+// same cap spilled in the walks and lost).
+#ifndef LSM_NN_WPE
+#define LSM_NN_WPE 8
+#endif
+#if LSM_NN_WPE > 0
 #define LSM_NN_ATTR __attribute__((amdgpu_waves_per_eu(LSM_NN_WPE)))
 #else
 #define LSM_NN_ATTR

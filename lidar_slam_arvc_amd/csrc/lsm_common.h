@@ -140,6 +140,34 @@ __device__ __forceinline__ float4 lsm_ld(const float4 *p, size_t i) {
 #endif
 }
 
+// Point readers of the grid walks: plain global loads (64-bit addresses), or buffer loads
+// through a descriptor of a cloud's points (a 32-bit offset per load; constant offsets of a load
+// group fold into the instructions). pt(k): point k; x(k): its x coordinate.
+struct GlobalPts {
+    const float4 *xyz;
+    __device__ __forceinline__ float4 pt(uint32_t k) const { return lsm_ld(xyz, k); }
+    __device__ __forceinline__ float x(uint32_t k) const {
+        return lsm_ld(reinterpret_cast<const float *>(xyz), size_t(k) * 4);
+    }
+};
+struct BufPts {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ float4 pt(uint32_t k) const {
+        typedef float v4 __attribute__((ext_vector_type(4)));
+        const v4 v = __builtin_bit_cast(v4, __builtin_amdgcn_raw_buffer_load_b128(r, int(k * 16u), 0, 0));
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+    __device__ __forceinline__ float x(uint32_t k) const {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, int(k * 16u), 0, 0));
+    }
+};
+// the descriptor of cloud C's points (C must be wave-uniform), its range covering the
+// LSM_XYZ_PAD spare points that prefetching walks may read
+__device__ __forceinline__ BufPts cloud_buf_pts(const CloudDev &C) {
+    return BufPts{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(C.xyz), 0,
+                                                    (C.n + LSM_XYZ_PAD) * 16, 0x00020000)};
+}
+
 __device__ __forceinline__ int lsm_clampi(int v, int lo, int hi) {
     return v < lo ? lo : (v > hi ? hi : v);
 }

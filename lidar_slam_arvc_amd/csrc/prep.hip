@@ -597,38 +597,13 @@ __device__ __forceinline__ void scan_run(const float4 *xyz, uint32_t a, uint32_t
 // scan_run with the window test folded into a predicate: body(p, k, in) is called for every
 // loaded point until the walk passes xh, `in` telling whether it lies in the window (fewer
 // divergent branches per point than nested ifs).
-// Point readers of the normals walks: plain global loads (64-bit addresses), or buffer loads
-// through a descriptor of the cloud's points (a 32-bit offset per load; the constant offsets of
-// a load group fold into the instructions), LSM_NORMALS_BUF.
-struct GlobalPts {
-    const float4 *xyz;
-    __device__ __forceinline__ float4 pt(uint32_t k) const { return lsm_ld(xyz, k); }
-    __device__ __forceinline__ float x(uint32_t k) const {
-        return lsm_ld(reinterpret_cast<const float *>(xyz), size_t(k) * 4);
-    }
-};
-struct BufPts {
-    __amdgpu_buffer_rsrc_t r;
-    __device__ __forceinline__ float4 pt(uint32_t k) const {
-        typedef float v4 __attribute__((ext_vector_type(4)));
-        const v4 v = __builtin_bit_cast(v4, __builtin_amdgcn_raw_buffer_load_b128(r, int(k * 16u), 0, 0));
-        return make_float4(v.x, v.y, v.z, v.w);
-    }
-    __device__ __forceinline__ float x(uint32_t k) const {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, int(k * 16u), 0, 0));
-    }
-};
+// point readers of the walks (GlobalPts / BufPts): lsm_common.h
 #ifndef LSM_NORMALS_BUF
 #define LSM_NORMALS_BUF 1
 #endif
 #if LSM_NORMALS_BUF
 typedef BufPts NormalsPts;
-// the descriptor of cloud C's points (C is wave-uniform in every normals kernel), its range
-// covering the LSM_XYZ_PAD spare points the prefetching walks may read
-__device__ __forceinline__ BufPts normals_pts(const CloudDev &C) {
-    return BufPts{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(C.xyz), 0,
-                                                    (C.n + LSM_XYZ_PAD) * 16, 0x00020000)};
-}
+__device__ __forceinline__ BufPts normals_pts(const CloudDev &C) { return cloud_buf_pts(C); }
 #else
 typedef GlobalPts NormalsPts;
 __device__ __forceinline__ GlobalPts normals_pts(const CloudDev &C) { return GlobalPts{C.xyz}; }
@@ -1299,7 +1274,12 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
 // Split launch, first half: the points predicted sparse (NL_SPARSE, no LDS). Deferred points are
 // appended to their cloud's dense list dlist[geo.pt_off + ...] (wave-aggregated; the order of
 // the list does not matter: every point's computation is independent of the others).
-#ifdef LSM_NSPARSE_WPE
+// registers of the sparse half capped for 8 waves per SIMD (64 VGPRs; 14 spilled outside the
+// walks): normals 148.2 -> 143.8 ms per step (7 waves: 144.1; uncapped, 80 VGPRs: 6 waves)
+#ifndef LSM_NSPARSE_WPE
+#define LSM_NSPARSE_WPE 8
+#endif
+#if LSM_NSPARSE_WPE > 0
 #define LSM_NSPARSE_ATTR __attribute__((amdgpu_waves_per_eu(LSM_NSPARSE_WPE)))
 #else
 #define LSM_NSPARSE_ATTR
