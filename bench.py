@@ -418,7 +418,7 @@ def main():
         npts = d0.kernel_stats("normals_points")["launches"]
         step_s = norm_ms / args.steps * 1e-3
         flops = 18.0 * nb + 150.0 * npts
-        valu = None
+        valu, valu_k = None, None
         vfile = os.path.join(ROOT, "profiles", "normals_valu.json")
         if os.path.exists(vfile) and not (ouster or loop):
             with open(vfile) as f:
@@ -426,15 +426,19 @@ def main():
             # PMC count of the same workload and normals mode
             if vj.get("pairs_per_gpu") == P and vj.get("normals_mode") == args.normals:
                 valu = vj.get("valu_per_step")
+                valu_k = {k: v.get("SQ_INSTS_VALU")
+                          for k, v in vj.get("per_kernel_per_step", {}).items()}
         ach = valu / step_s / 1e9 if valu else None
         roof_n = {"bound": "valu", "kernel": ("lazy_normals_kernel (the target normals each ICP "
                                               "pass reaches)" if args.normals == "lazy" else
-                                              "normals_kernel (one launch per step)") +
+                                              "normals_sparse_kernel + normals_dense_kernel "
+                                              "(the split launch, once per step)") +
                                              ": hybrid kNN-300 / r 0.3 m",
                   "mode": args.normals, "unit": "G wave-instructions/s",
                   "achieved": round(ach, 2) if ach else None, "peak": VALU_ISSUE_PEAK_G,
                   "frac": round(ach / VALU_ISSUE_PEAK_G, 5) if ach else None,
                   "valu_instructions_per_step": valu,
+                  "valu_instructions_per_kernel": valu_k,
                   "ms_per_step": round(step_s * 1e3, 4),
                   "launches_per_step": (stats["normals"]["launches"] +
                                         stats["normals_lazy"]["launches"]) / args.steps,
