@@ -1276,6 +1276,47 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
 // the list does not matter: every point's computation is independent of the others).
 // registers of the sparse half capped for 8 waves per SIMD (64 VGPRs; 14 spilled outside the
 // walks): normals 148.2 -> 143.8 ms per step (7 waves: 144.1; uncapped, 80 VGPRs: 6 waves)
+#ifndef LSM_NORMALS_WG_APPEND
+#define LSM_NORMALS_WG_APPEND 1
+#endif
+
+// Append point j (when `take`) to a cloud's list, one atomic per workgroup: the workgroup's
+// entries stay one run in lane order. Every thread of the workgroup must call it.
+__device__ __forceinline__ void wg_append(bool take, uint32_t j, uint32_t *list, uint32_t *cnt) {
+    __shared__ uint32_t s_cnt[PT_THREADS / LSM_WAVE + 1];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t bm = __ballot(take);
+    if (lane == 0) s_cnt[w] = uint32_t(__popcll(bm));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int q = 0; q < PT_THREADS / LSM_WAVE; ++q) tot += s_cnt[q];
+        s_cnt[PT_THREADS / LSM_WAVE] = tot ? atomicAdd(cnt, tot) : 0u;
+    }
+    __syncthreads();
+    if (take) {
+        uint32_t base = s_cnt[PT_THREADS / LSM_WAVE];
+        for (int q = 0; q < w; ++q) base += s_cnt[q];
+        list[base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = j;
+    }
+    __syncthreads();   // s_cnt is reused by the next call
+}
+
+// Split launch, stage 0 (LSM_NORMALS_CLASSIFY): the clouds' points into a sparse list and a
+// dense list by the density prediction, so the sparse half also runs in full waves.
+__global__ void __launch_bounds__(PT_THREADS)
+normals_classify_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
+                        uint32_t *slist, uint32_t *scnt, uint32_t *dlist, uint32_t *dcnt) {
+    const Seg s = segs[blockIdx.x];
+    const CloudDev C = cd[s.cloud];
+    const int j = s.start + threadIdx.x;
+    bool dense = false;
+    const bool valid = j < C.n;
+    if (valid) dense = predict_dense(C, np, lsm_ld(C.xyz, j));
+    const uint32_t off = geo[s.cloud].pt_off;
+    wg_append(valid && !dense, uint32_t(j), slist + off, scnt + s.cloud);
+    wg_append(valid && dense, uint32_t(j), dlist + off, dcnt + s.cloud);
+}
 #ifndef LSM_NSPARSE_WPE
 #define LSM_NSPARSE_WPE 8
 #endif
@@ -1284,15 +1325,23 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
 #else
 #define LSM_NSPARSE_ATTR
 #endif
-template <int G>
+template <int G, bool LIST = false>
 __global__ void __launch_bounds__(PT_THREADS) LSM_NSPARSE_ATTR
 normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
-                      uint32_t *dlist, uint32_t *dcnt, unsigned long long *stats) {
+                      uint32_t *dlist, uint32_t *dcnt, unsigned long long *stats,
+                      const uint32_t *slist = nullptr, const uint32_t *scnt = nullptr) {
     const Seg s = segs[blockIdx.x];
     const CloudDev C = cd[s.cloud];
-    const int j = s.start + threadIdx.x;
+    int j = s.start + threadIdx.x;
+    bool valid = j < C.n;
+    if (LIST) {   // LSM_NORMALS_CLASSIFY: entries of the cloud's sparse list
+        const uint32_t n = scnt[s.cloud];
+        if (uint32_t(s.start) >= n) return;   // the whole workgroup is past the list
+        valid = uint32_t(j) < n;
+        if (valid) j = int(slist[geo[s.cloud].pt_off + uint32_t(j)]);
+    }
     bool defer = false;
-    if (j < C.n) {
+    if (valid) {
         const float4 q = lsm_ld(C.xyz, j);
         CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                    C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
@@ -1300,8 +1349,15 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
         if (stats && !defer) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
     }
     const uint64_t bm = __ballot(defer);
+    const int lane = threadIdx.x & 63;
+#if LSM_NORMALS_WG_APPEND
+    // one append per workgroup: its deferred points stay one run in cell order (the dense
+    // half's waves then hold neighbouring points)
+    (void)bm;
+    (void)lane;
+    wg_append(defer, uint32_t(j), dlist + geo[s.cloud].pt_off, dcnt + s.cloud);
+#else
     if (bm) {
-        const int lane = threadIdx.x & 63;
         const int leader = __ffsll((unsigned long long)bm) - 1;
         uint32_t base = 0;
         if (lane == leader) base = atomicAdd(dcnt + s.cloud, uint32_t(__popcll(bm)));
@@ -1309,6 +1365,7 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
         if (defer)
             dlist[geo[s.cloud].pt_off + base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = uint32_t(j);
     }
+#endif
 }
 
 // Split launch, second half: one lane per entry of the clouds' dense lists (NL_DENSE), so the
@@ -2132,7 +2189,15 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                     const char *e = getenv("LSM_NORMALS_GD");
                     return e ? atoi(e) : NORMALS_GD_DEFAULT;
                 }();
-                if (G == 4)
+                const char *cl = getenv("LSM_NORMALS_CLASSIFY");   // read per call
+                if (cl && atoi(cl) != 0) {
+                    uint32_t *slist = (uint32_t *)ctx->buf("n_slist", N * 4);
+                    uint32_t *scnt = (uint32_t *)ctx->buf("n_scnt", size_t(K) * 4);
+                    if (!slist || !scnt) return LSM_ENOMEM;
+                    LSM_HIP_TRY(ctx, hipMemsetAsync(scnt, 0, size_t(K) * 4, st));
+                    normals_classify_kernel<<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, slist, scnt, dlist, dcnt);
+                    normals_sparse_kernel<2, true><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns, slist, scnt);
+                } else if (G == 4)
                     normals_sparse_kernel<4><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
                 else
                     normals_sparse_kernel<2><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);

@@ -130,7 +130,8 @@ def test_normals_preclassification_bit_identical(dev, seq64k, max_nn, monkeypatc
 def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
     """The split launch (default: the points predicted sparse, then every deferred point in
     full waves of the clouds' dense lists; its dense half with per-lane walks or with the
-    wave-cooperative scans, LSM_NORMALS_COOP) against the one-kernel launch (LSM_NORMALS_SPLIT=0):
+    wave-cooperative scans, LSM_NORMALS_COOP; its sparse half over a pre-classified list,
+    LSM_NORMALS_CLASSIFY) against the one-kernel launch (LSM_NORMALS_SPLIT=0):
     bit-identical normals on bench scans, under heavier truncation, on degenerate neighbourhoods
     (duplicates saturating a u8 bin, a dense patch) and on clouds that carry prior normals
     (EstimateNormals re-run on a cloud with normals orients to them)."""
@@ -143,22 +144,23 @@ def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
     keep = _lib.prep_params(max_nn=max_nn, min_radius=-np.inf, max_radius=1e15,
                             min_height=-1e15, max_height=1e15)
     out = {}
-    for split, coop in (("1", "0"), ("1", "1"), ("0", "0")):
+    for split, coop, cls in (("1", "0", "0"), ("1", "1", "0"), ("1", "0", "1"), ("0", "0", "0")):
         monkeypatch.setenv("LSM_NORMALS_SPLIT", split)
         monkeypatch.setenv("LSM_NORMALS_COOP", coop)
+        monkeypatch.setenv("LSM_NORMALS_CLASSIFY", cls)
         ids = [dev.upload(c) for c in clouds]
         try:
             dev.preprocess(ids, prm)
             first = [dev.download(i, normals=True)[1] for i in ids]
             dev.preprocess(ids, keep)          # again, now with prior normals
             second = [dev.download(i, normals=True)[1] for i in ids]
-            out[split + coop] = first + second
+            out[split + coop + cls] = first + second
         finally:
             _release(dev, ids)
-    monkeypatch.delenv("LSM_NORMALS_SPLIT")
-    monkeypatch.delenv("LSM_NORMALS_COOP")
-    for variant in ("10", "11"):
-        for a, b in zip(out[variant], out["00"]):
+    for v in ("LSM_NORMALS_SPLIT", "LSM_NORMALS_COOP", "LSM_NORMALS_CLASSIFY"):
+        monkeypatch.delenv(v)
+    for variant in ("100", "110", "101"):
+        for a, b in zip(out[variant], out["000"]):
             assert np.array_equal(a, b), variant
 
 
