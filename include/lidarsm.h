@@ -126,6 +126,12 @@ int lsm_preprocess_batch(lsm_ctx *ctx, int64_t n, const lsm_cloud *clouds,
 int lsm_cloud_download(lsm_ctx *ctx, lsm_cloud cloud, double *xyz, double *normals, int64_t cap);
 /* Voxel keys (int32 x 3 per output point, Open3D voxel_index) of a voxelised cloud. */
 int lsm_cloud_voxel_keys(lsm_ctx *ctx, lsm_cloud cloud, int32_t *keys, int64_t cap);
+/* Diagnostics (no reference counterpart): the device layout of a processed cloud -- perm[i] =
+ * reference-order index of sorted point i (cap >= n rows), and the cell table (cell_start, the
+ * first sorted position of every blocked cell, ncells + 1 entries; cells may be NULL). *ncells
+ * receives the number of cells. The tests compare the grid builds with it. */
+int lsm_cloud_layout(lsm_ctx *ctx, lsm_cloud cloud, int32_t *perm, int64_t cap, uint32_t *cells,
+                     int64_t cell_cap, int64_t *ncells);
 
 /* Registration (KeyFrame.local_registration_simple, keyframe.py:231-260) --------------------
  * src = `other` (keyframe j), tgt = `self` (keyframe i); the result maps src into tgt frame. */

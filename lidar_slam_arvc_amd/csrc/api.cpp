@@ -590,6 +590,32 @@ int lsm_cloud_voxel_keys(lsm_ctx *ctx, lsm_cloud cloud, int32_t *keys, int64_t c
     return LSM_OK;
 }
 
+int lsm_cloud_layout(lsm_ctx *ctx, lsm_cloud cloud, int32_t *perm, int64_t cap, uint32_t *cells,
+                     int64_t cell_cap, int64_t *ncells) {
+    if (!ctx || !ncells) return LSM_EINVAL;
+    Cloud *c = find_cloud(ctx, cloud);
+    if (!c) {
+        ctx->set_error("unknown cloud handle");
+        return LSM_EINVAL;
+    }
+    if (!c->processed) {
+        ctx->set_error("cloud is not processed");
+        return LSM_ESTATE;
+    }
+    const int64_t nc = int64_t(c->dev.nbx) * c->dev.nby * c->dev.nbz * LSM_BLK_CELLS;
+    *ncells = nc;
+    if ((perm && cap < c->n) || (cells && cell_cap < nc + 1)) return LSM_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    if (perm && c->n > 0)
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(perm, c->d_perm, size_t(c->n) * 4, hipMemcpyDeviceToHost,
+                                        ctx->stream));
+    if (cells)
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(cells, c->d_cell, size_t(nc + 1) * 4,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return LSM_OK;
+}
+
 static int check_icp(lsm_ctx *ctx, const lsm_icp_params *p) {
     if (!p) return LSM_EINVAL;
     if (!(p->max_correspondence_distance > 0.0)) {

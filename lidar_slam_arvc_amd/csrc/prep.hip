@@ -225,6 +225,30 @@ voxel_reduce(const uint64_t *skeys, const uint32_t *svals, const uint32_t *vid_e
     vcloud[o] = c;
 }
 
+// vb[k] = vid[pstart[k]]: the first voxel id of cloud k (k = K: the voxel total)
+__global__ void vox_cloud_bounds(const uint32_t *vid, const uint32_t *pstart, int n, uint32_t *vb) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) vb[k] = vid[pstart[k]];
+}
+
+// voxel o's f64 centroid and int32 key into its cloud's arrays (voff: the cloud's first voxel)
+__global__ void vox_scatter(const double *cent, const int32_t *vkeys, const int32_t *vcloud,
+                            uint32_t nvox, const uint32_t *voff, double *const *cp,
+                            int32_t *const *kp) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= nvox) return;
+    const int c = vcloud[o];
+    const uint32_t l = o - voff[c];
+    double *dc = cp[c] + size_t(l) * 3;
+    int32_t *dk = kp[c] + size_t(l) * 3;
+    dc[0] = cent[3 * size_t(o)];
+    dc[1] = cent[3 * size_t(o) + 1];
+    dc[2] = cent[3 * size_t(o) + 2];
+    dk[0] = vkeys[3 * size_t(o)];
+    dk[1] = vkeys[3 * size_t(o) + 1];
+    dk[2] = vkeys[3 * size_t(o) + 2];
+}
+
 __global__ void point_cloud_ids(const uint32_t *cloud_off, const uint32_t *cloud_n, int ncloud,
                                 int32_t *pt_cloud) {
     int c = blockIdx.y;
@@ -251,6 +275,12 @@ __device__ __forceinline__ int cell_coord(float v, float o, float inv, int nmax)
     return lsm_clampi((int)floorf((v - o) * inv), 0, nmax - 1);
 }
 
+// x as an order-preserving u32 (IEEE sign flip)
+__device__ __forceinline__ uint32_t x_key(float x) {
+    const uint32_t xb = __float_as_uint(x);
+    return (xb & 0x80000000u) ? ~xb : (xb | 0x80000000u);
+}
+
 __global__ void __launch_bounds__(PT_THREADS)
 grid_keys(const Seg *segs, const float4 *pts, const GridGeo *geo, uint64_t *keys,
           uint32_t *vals) {
@@ -265,9 +295,8 @@ grid_keys(const Seg *segs, const float4 *pts, const GridGeo *geo, uint64_t *keys
     int cz = cell_coord(p.z, G.oz, G.inv_cell, G.nz);
     // (cell, x) key: inside a cell points are ordered by x, which lets the correspondence search
     // walk a cell outwards from the query's x and stop once dx^2 exceeds the best distance
-    uint32_t xb = __float_as_uint(p.x);
-    xb = (xb & 0x80000000u) ? ~xb : (xb | 0x80000000u);
-    keys[g] = (uint64_t(G.cell_off + uint32_t(lsm_cell_lin(G.nbx, G.nby, cx, cy, cz))) << 32) | xb;
+    keys[g] = (uint64_t(G.cell_off + uint32_t(lsm_cell_lin(G.nbx, G.nby, cx, cy, cz))) << 32) |
+              x_key(p.x);
     vals[g] = g;
 }
 
@@ -864,6 +893,10 @@ struct NPhase {
 //              (coop_visit); every lane of the wave must call it (`act` false: no point).
 // Returns false when the point was deferred.
 constexpr int NL_AUTO = 0, NL_SPARSE = 1, NL_DENSE = 2, NL_COOP = 3;
+#ifndef LSM_NDIAG
+#define LSM_NDIAG 0   // diagnostics builds only (wrong normals): 1 / 3 stop the dense half after
+                      // scan 1 (3: without its histogram adds), 2 before its final pass
+#endif
 
 // wave-uniform min / max (readfirstlane: the result is known uniform, an SGPR value)
 __device__ __forceinline__ int wave_uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -1018,7 +1051,11 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                 NP_ST(ph, 1, 1u);
                 if (!dense) acc.add(p, k);
                 ++count;
+#if LSM_NDIAG == 3   // diagnostics build: no histogram adds (the walk's own cost)
+                count += bb & 1;
+#else
                 lds_add(R.at(bb >> 2), 1u << ((bb & 3) << 3));   // u8 bin, carries detected below
+#endif
             }
     };
     if (MODE == NL_COOP) {
@@ -1036,6 +1073,13 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         acc.finish();
         return true;
     }
+#if LSM_NDIAG == 1 || LSM_NDIAG == 3
+    if constexpr (MODE == NL_DENSE) {   // diagnostics build: the dense half stops after scan 1
+        acc.c.n = count;
+        acc.finish();
+        return true;
+    }
+#endif
     double top = np.r2;   // every point below or member has d2 <= top (up to rounding)
     uint32_t need = uint32_t(np.max_nn);   // still to take from the members
     if (count <= np.max_nn) {
@@ -1149,6 +1193,13 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     // d2 below min(r2, dlo, the chosen d2 bin's lower edge) is certainly "below", d2 above
     // max(dhi-side bounds) certainly "above"; only the band between takes the exact f64 test
     // (the f32 d2 is within 4.2e-7 relative; 2e-6 of margin).
+#if LSM_NDIAG == 2
+    if constexpr (MODE == NL_DENSE) {   // diagnostics build: the dense half stops before the final pass
+        acc.c.n = count + int(need) + int(top * 1e6);
+        acc.finish();
+        return true;
+    }
+#endif
     float below32, above32;
     sel_thresholds(S, np, below32, above32);
     uint32_t m = 0;
@@ -1924,16 +1975,20 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
                                 rocprim::plus<uint32_t>(), st));
         voxel_reduce<<<nb, PT_THREADS, 0, st>>>(k_out, v_out, vid, flag, ntot, *pts, ptc, d_geo,
                                                 cent, vkeys, vpts, vcloud);
+        // voxels per cloud: the sort keeps each cloud's keys together (key_off), so cloud k's
+        // voxel ids run from vid[P_k] to vid[P_k+1], P_k = the points of the clouds before it
+        std::vector<uint32_t> pstart(size_t(K) + 1, 0);
+        for (int k = 0; k < K; ++k) pstart[k + 1] = pstart[k] + cnt[k];
+        uint32_t *d_pstart, *d_vb = (uint32_t *)ctx->buf("v_vb", (size_t(K) + 1) * 4);
+        if (!d_vb) return LSM_ENOMEM;
+        if ((rc = upload_vec(ctx, "v_pstart", pstart, &d_pstart))) return rc;
+        vox_cloud_bounds<<<(K + 1 + 255) / 256, 256, 0, st>>>(vid, d_pstart, K + 1, d_vb);
         ctx->toc("voxel", ev);
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(&nvox, vid + ntot, 4, hipMemcpyDeviceToHost, st));
+        std::vector<uint32_t> vb(size_t(K) + 1);
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(vb.data(), d_vb, vb.size() * 4, hipMemcpyDeviceToHost, st));
         LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-        std::vector<int32_t> vc(nvox);
-        if (nvox) {
-            LSM_HIP_TRY(ctx, hipMemcpyAsync(vc.data(), vcloud, size_t(nvox) * 4,
-                                            hipMemcpyDeviceToHost, st));
-            LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-        }
-        for (uint32_t i = 0; i < nvox; ++i) vcount[vc[i]]++;
+        nvox = vb[K];
+        for (int k = 0; k < K; ++k) vcount[k] = vb[k + 1] - vb[k];
     }
     uint32_t run = 0;
     for (int k = 0; k < K; ++k) {
@@ -1955,12 +2010,21 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
                 return LSM_ENOMEM;
             }
         }
-        if (cnt[k]) {
-            LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_vox, cent + size_t(off[k]) * 3, size_t(cnt[k]) * 24,
-                                            hipMemcpyDeviceToDevice, st));
-            LSM_HIP_TRY(ctx, hipMemcpyAsync(c->d_vkeys, vkeys + size_t(off[k]) * 3,
-                                            size_t(cnt[k]) * 12, hipMemcpyDeviceToDevice, st));
+    }
+    if (nvox) {   // every cloud's f64 centroids and keys in one launch (not 2 K copies)
+        std::vector<double *> cp(K);
+        std::vector<int32_t *> kp(K);
+        for (int k = 0; k < K; ++k) {
+            cp[k] = clouds[k]->d_vox;
+            kp[k] = clouds[k]->d_vkeys;
         }
+        double **d_cp;
+        int32_t **d_kp;
+        uint32_t *d_voff;
+        if ((rc = upload_vec(ctx, "v_cp", cp, &d_cp))) return rc;
+        if ((rc = upload_vec(ctx, "v_kp", kp, &d_kp))) return rc;
+        if ((rc = upload_vec(ctx, "v_voff", off, &d_voff))) return rc;
+        vox_scatter<<<(nvox + 255) / 256, 256, 0, st>>>(cent, vkeys, vcloud, nvox, d_voff, d_cp, d_kp);
     }
     *pts = vpts;
     return LSM_OK;
@@ -2106,6 +2170,8 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     }
     ctx->tic("grid", &ev);
     LSM_HIP_TRY(ctx, hipMemsetAsync(nonempty, 0, size_t(K) * 4, st));
+    int64_t maxcells1 = 0;
+    for (int k = 0; k < K; ++k) maxcells1 = std::max<int64_t>(maxcells1, int64_t(geo[k].ncells) + 1);
     if (!psegs.empty()) {
         grid_keys<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, wpts, d_geo, k_in, v_in);
         size_t tmpb = 0;
@@ -2118,10 +2184,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                                                               wpts, d_perm_ptrs, nonempty);
     }
     {
-        int64_t maxcells = 0;
-        for (int k = 0; k < K; ++k)
-            maxcells = std::max<int64_t>(maxcells, int64_t(geo[k].ncells) + 1);
-        const int gx = int(std::min<int64_t>((maxcells + FILL_TILE - 1) / FILL_TILE, 4096));
+        const int gx = int(std::min<int64_t>((maxcells1 + FILL_TILE - 1) / FILL_TILE, 4096));
         grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs);
     }
     ctx->toc("grid", ev);

@@ -164,6 +164,42 @@ def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
             assert np.array_equal(a, b), variant
 
 
+@pytest.mark.parametrize("voxel", [0.0, 0.1])
+def test_grid_layout_invariants(dev, seq64k, voxel):
+    """The device layout (lsm_cloud_layout) of clouds pre-processed as one batch -- bench scans,
+    an empty cloud, exact duplicates and signed zeros: perm is a permutation, the cell table
+    rises from 0 to n, and inside every cell the points are sorted by x with x ties in reference
+    order (the stable (cell, x) radix order the searches and their tie-breaking rely on), every
+    cell spatially compact."""
+    rng = np.random.default_rng(5)
+    dup = np.repeat([[3.0, 1.0, 0.2], [-0.0, 2.0, 0.1], [0.0, 2.0, 0.1]], 7, axis=0)
+    ties = np.r_[dup, np.c_[rng.uniform(-4, 4, 3000), rng.uniform(-4, 4, 3000),
+                            rng.uniform(-0.5, 0.5, 3000)]].astype(np.float32)
+    clouds = list(seq64k.scans[:3]) + [np.zeros((0, 3), np.float32), ties]
+    keep = dict(min_radius=-np.inf, max_radius=1e15, min_height=-1e15, max_height=1e15)
+    ids = [dev.upload(c) for c in clouds]
+    try:
+        dev.preprocess(ids, _lib.prep_params(voxel_size=voxel or None, **keep))
+        for h in ids:
+            perm, cells = dev.layout(h)
+            pts = dev.download(h).astype(np.float32)
+            n = len(pts)
+            assert np.array_equal(np.sort(perm), np.arange(n))
+            assert cells[0] == 0 and cells[-1] == n and np.all(np.diff(cells.astype(np.int64)) >= 0)
+            sp = pts[perm]
+            occ = np.flatnonzero(np.diff(cells.astype(np.int64)) > 0)
+            for c in occ:
+                a, b = int(cells[c]), int(cells[c + 1])
+                x = sp[a:b, 0]
+                dx = np.diff(x)
+                assert np.all(dx >= 0)
+                assert np.all(np.diff(perm[a:b])[dx == 0] > 0)   # x ties in reference order
+                ext = sp[a:b].max(0) - sp[a:b].min(0)
+                assert np.all(ext <= 0.5), ext
+    finally:
+        _release(dev, ids)
+
+
 def test_normals_degenerate_neighbourhoods(dev):
     """kNN-300 truncation on pathological neighbourhoods: 400 exact duplicates of one point (one
     d2 value holds more than a u8 histogram bin can count and more than the selection buffer
