@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <type_traits>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <vector>
@@ -124,36 +125,72 @@ filter_write(const Seg *segs, const float *const *raw, const int32_t *nraw, Filt
 // ------------------------------------------------------------------------------------------
 // bounding boxes (f64 for the voxel grid, f32 values are exact in f64)
 // ------------------------------------------------------------------------------------------
+// Several workgroups per cloud (one workgroup per cloud left the GPU mostly idle: 0.22 ms per
+// 257-cloud batch): wave min / max in f32, then one atomic per wave on order-preserving u32 keys
+// (bbk: 6 per cloud, min slots start at ~0, max slots at 0); bbox_final turns them into the f64
+// box (f32 values are exact in f64). Min / max are order-independent, so the box is the same.
+constexpr int BBOX_BLOCKS = 16;   // workgroups per cloud
+__device__ __forceinline__ uint32_t f32_key(float v) {
+    const uint32_t b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float key_f32(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
 __global__ void __launch_bounds__(256)
-bbox_kernel(const float4 *pts, const uint32_t *cloud_off, const uint32_t *cloud_n, double *bb) {
+bbox_kernel(const float4 *pts, const uint32_t *cloud_off, const uint32_t *cloud_n, uint32_t *bbk) {
     const int c = blockIdx.x;
     const uint32_t off = cloud_off[c], n = cloud_n[c];
-    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        float4 p = pts[off + i];
-        mn[0] = fmin(mn[0], (double)p.x);
-        mn[1] = fmin(mn[1], (double)p.y);
-        mn[2] = fmin(mn[2], (double)p.z);
-        mx[0] = fmax(mx[0], (double)p.x);
-        mx[1] = fmax(mx[1], (double)p.y);
-        mx[2] = fmax(mx[2], (double)p.z);
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = blockIdx.y * blockDim.x + threadIdx.x; i < n; i += gridDim.y * blockDim.x) {
+        const float4 p = pts[off + i];
+        mn[0] = fminf(mn[0], p.x);
+        mn[1] = fminf(mn[1], p.y);
+        mn[2] = fminf(mn[2], p.z);
+        mx[0] = fmaxf(mx[0], p.x);
+        mx[1] = fmaxf(mx[1], p.y);
+        mx[2] = fmaxf(mx[2], p.z);
     }
-    __shared__ double red[6][256];
-    for (int k = 0; k < 3; ++k) {
-        red[k][threadIdx.x] = mn[k];
-        red[3 + k][threadIdx.x] = mx[k];
-    }
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            for (int k = 0; k < 3; ++k) {
-                red[k][threadIdx.x] = fmin(red[k][threadIdx.x], red[k][threadIdx.x + s]);
-                red[3 + k][threadIdx.x] = fmax(red[3 + k][threadIdx.x], red[3 + k][threadIdx.x + s]);
-            }
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        for (int o = 32; o > 0; o >>= 1) {
+            mn[k] = fminf(mn[k], __shfl_xor(mn[k], o, LSM_WAVE));
+            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], o, LSM_WAVE));
         }
-        __syncthreads();
+    if ((threadIdx.x & 63) == 0 && mn[0] <= mx[0]) {
+        for (int k = 0; k < 3; ++k) {
+            atomicMin(bbk + 6 * c + k, f32_key(mn[k]));
+            atomicMax(bbk + 6 * c + 3 + k, f32_key(mx[k]));
+        }
     }
-    if (threadIdx.x < 6) bb[6 * c + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void bbox_init(uint32_t *bbk, int K) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 6 * K) bbk[i] = (i % 6) < 3 ? 0xffffffffu : 0u;
+}
+
+// an empty cloud keeps (+inf, -inf) as the one-workgroup kernel left it
+__global__ void bbox_final(const uint32_t *bbk, int K, double *bb) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 6 * K) return;
+    const uint32_t k = bbk[i];
+    const bool lo = (i % 6) < 3;
+    bb[i] = (lo && k == 0xffffffffu) ? INFINITY : ((!lo && k == 0u) ? -INFINITY : double(key_f32(k)));
+}
+
+// bb[6 k .. 6 k + 6) = (min xyz, max xyz) of cloud k
+int run_bbox(lsm_ctx *ctx, const float4 *pts, const uint32_t *d_off, const uint32_t *d_cnt, int K,
+             double *d_bb, const char *name) {
+    hipStream_t st = ctx->stream;
+    uint32_t *bbk = (uint32_t *)ctx->buf(name, size_t(K) * 24 + 4);
+    if (!bbk) return LSM_ENOMEM;
+    const int g = (6 * K + 255) / 256;
+    bbox_init<<<g, 256, 0, st>>>(bbk, K);
+    bbox_kernel<<<dim3(K, BBOX_BLOCKS), 256, 0, st>>>(pts, d_off, d_cnt, bbk);
+    bbox_final<<<g, 256, 0, st>>>(bbk, K, d_bb);
+    return LSM_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -165,9 +202,11 @@ struct VoxGeo {         // per cloud, computed on the host from the f64 bbox
     uint64_t key_off;   // offset of this cloud in the global key space
 };
 
+// KeyT: uint32_t when the batch's key space fits 32 bits (4 radix passes over 4-byte keys)
+template <typename KeyT>
 __global__ void __launch_bounds__(PT_THREADS)
 voxel_keys(const Seg *segs, const float4 *pts, const uint32_t *cloud_off, const uint32_t *cloud_n,
-           const VoxGeo *geo, double v, uint64_t *keys, uint32_t *vals) {
+           const VoxGeo *geo, double v, KeyT *keys, uint32_t *vals) {
     const Seg s = segs[blockIdx.x];
     const int i = s.start + threadIdx.x;
     if (i >= int(cloud_n[s.cloud])) return;
@@ -178,36 +217,72 @@ voxel_keys(const Seg *segs, const float4 *pts, const uint32_t *cloud_off, const 
     int64_t kx = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.x, G.ox), v));
     int64_t ky = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.y, G.oy), v));
     int64_t kz = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.z, G.oz), v));
-    keys[g] = G.key_off + uint64_t((kx * G.dy + ky) * G.dz + kz);
+    keys[g] = KeyT(G.key_off + uint64_t((kx * G.dy + ky) * G.dz + kz));
     vals[g] = g;
 }
 
 // One thread per sorted entry; voxel heads sum their members in index order (stable sort keeps
 // the original order inside a voxel) exactly like AccumulatedPoint::AddPoint.
+template <typename KeyT>
 __global__ void __launch_bounds__(PT_THREADS)
-voxel_flags(const uint64_t *skeys, uint32_t n, uint32_t *flag) {
+voxel_flags(const KeyT *skeys, uint32_t n, uint32_t *flag) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     flag[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? 1u : 0u;
 }
 
+// vstart[vid[i]] = i for every voxel head i, and vstart[nvox] = n: voxel o's members are the
+// sorted entries [vstart[o], vstart[o + 1])
 __global__ void __launch_bounds__(PT_THREADS)
-voxel_reduce(const uint64_t *skeys, const uint32_t *svals, const uint32_t *vid_excl,
-             const uint32_t *flag, uint32_t n, const float4 *pts, const int32_t *pt_cloud,
+voxel_heads(const uint32_t *flag, const uint32_t *vid_excl, uint32_t n, uint32_t *vstart) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (flag[i]) vstart[vid_excl[i]] = i;
+    if (i == 0) vstart[vid_excl[n]] = n;
+}
+
+// One thread per voxel (the grid covers n threads; those past the voxel count exit): the members
+// summed in index order, as AccumulatedPoint::AddPoint does -- the same left fold in f64 as one
+// thread per head walking its run, with the member loads issued four at a time (the run's length
+// is known from vstart, so the loads need not wait for the run-end test).
+template <typename KeyT>
+__global__ void __launch_bounds__(PT_THREADS)
+voxel_reduce(const KeyT *skeys, const uint32_t *svals, const uint32_t *vid_excl,
+             const uint32_t *vstart, uint32_t n, const float4 *pts, const int32_t *pt_cloud,
              const VoxGeo *geo, double *cent, int32_t *vkeys, float4 *vpts, int32_t *vcloud) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !flag[i]) return;
-    const uint64_t key = skeys[i];
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= vid_excl[n]) return;
+    const uint32_t i = vstart[o], e = vstart[o + 1];
     double sx = 0.0, sy = 0.0, sz = 0.0;
     uint32_t j = i;
-    for (; j < n && skeys[j] == key; ++j) {
-        float4 p = pts[svals[j]];
+    // long runs (voxels of thousands of points near the sensor set the kernel's duration: one
+    // dependent chain each) in batches of 16 loads in flight
+    for (; j + 16 <= e; j += 16) {
+        float4 p[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[q] = pts[svals[j + q]];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            sx = lsm_dadd(sx, (double)p[q].x);
+            sy = lsm_dadd(sy, (double)p[q].y);
+            sz = lsm_dadd(sz, (double)p[q].z);
+        }
+    }
+    for (; j + 4 <= e; j += 4) {
+        const uint32_t v0 = svals[j], v1 = svals[j + 1], v2 = svals[j + 2], v3 = svals[j + 3];
+        const float4 p0 = pts[v0], p1 = pts[v1], p2 = pts[v2], p3 = pts[v3];
+        sx = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sx, (double)p0.x), (double)p1.x), (double)p2.x), (double)p3.x);
+        sy = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sy, (double)p0.y), (double)p1.y), (double)p2.y), (double)p3.y);
+        sz = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sz, (double)p0.z), (double)p1.z), (double)p2.z), (double)p3.z);
+    }
+    for (; j < e; ++j) {
+        const float4 p = pts[svals[j]];
         sx = lsm_dadd(sx, (double)p.x);
         sy = lsm_dadd(sy, (double)p.y);
         sz = lsm_dadd(sz, (double)p.z);
     }
-    const double cnt = double(j - i);
-    const uint32_t o = vid_excl[i];
+    const uint64_t key = uint64_t(skeys[i]);
+    const double cnt = double(e - i);
     const double cx = lsm_ddiv(sx, cnt), cy = lsm_ddiv(sy, cnt), cz = lsm_ddiv(sz, cnt);
     cent[3 * o] = cx;
     cent[3 * o + 1] = cy;
@@ -1385,6 +1460,8 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
     const CloudDev C = cd[s.cloud];
     int j = s.start + threadIdx.x;
     bool valid = j < C.n;
+    // lazy completion: a point whose normal an earlier per-point batch computed is skipped
+    if (!LIST && valid && C.nstate && C.nstate[j]) valid = false;
     if (LIST) {   // LSM_NORMALS_CLASSIFY: entries of the cloud's sparse list
         const uint32_t n = scnt[s.cloud];
         if (uint32_t(s.start) >= n) return;   // the whole workgroup is past the list
@@ -1894,7 +1971,7 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
     if ((rc = upload_vec(ctx, "v_cnt", cnt, &d_cnt))) return rc;
     double *d_bb = (double *)ctx->buf("v_bb", size_t(K) * 48);
     if (!d_bb) return LSM_ENOMEM;
-    bbox_kernel<<<K, 256, 0, st>>>(*pts, d_off, d_cnt, d_bb);
+    if ((rc = run_bbox(ctx, *pts, d_off, d_cnt, K, d_bb, "v_bbk"))) return rc;
     std::vector<double> bb(size_t(K) * 6);
     LSM_HIP_TRY(ctx, hipMemcpyAsync(bb.data(), d_bb, bb.size() * 8, hipMemcpyDeviceToHost, st));
     LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
@@ -1940,12 +2017,13 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
     uint32_t *v_out = (uint32_t *)ctx->buf("v_vout", N * 4);
     uint32_t *flag = (uint32_t *)ctx->buf("v_flag", N * 4 + 4);
     uint32_t *vid = (uint32_t *)ctx->buf("v_vid", N * 4 + 4);
+    uint32_t *vstart = (uint32_t *)ctx->buf("v_vstart", N * 4 + 4);
     int32_t *ptc = (int32_t *)ctx->buf("v_ptc", N * 4);
     double *cent = (double *)ctx->buf("v_cent", N * 24);
     int32_t *vkeys = (int32_t *)ctx->buf("v_keys", N * 12);
     float4 *vpts = (float4 *)ctx->buf("v_pts", N * 16);
     int32_t *vcloud = (int32_t *)ctx->buf("v_vcloud", N * 4);
-    if (!k_in || !k_out || !v_in || !v_out || !flag || !vid || !ptc || !cent || !vkeys || !vpts ||
+    if (!k_in || !k_out || !v_in || !v_out || !flag || !vid || !vstart || !ptc || !cent || !vkeys || !vpts ||
         !vcloud) {
         ctx->set_error("scratch allocation failed (voxel)");
         return LSM_ENOMEM;
@@ -1955,26 +2033,38 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
     if (!segs.empty()) {
         hipEvent_t ev;
         ctx->tic("voxel", &ev);
-        voxel_keys<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, *pts, d_off, d_cnt, d_geo, v,
-                                                           k_in, v_in);
         point_cloud_ids<<<dim3(64, K), 256, 0, st>>>(d_off, d_cnt, K, ptc);
         const int endbit = bits_for(key_off);
-        size_t tmpb = 0;
-        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(nullptr, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit,
-                                  st));
-        void *tmp = ctx->buf("sort_tmp", tmpb);
-        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(tmp, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit, st));
         const int nb = int((ntot + PT_THREADS - 1) / PT_THREADS);
-        voxel_flags<<<nb, PT_THREADS, 0, st>>>(k_out, ntot, flag);
-        LSM_HIP_TRY(ctx, hipMemsetAsync(flag + ntot, 0, 4, st));
-        tmpb = 0;
-        LSM_HIP_TRY(ctx, rocprim::exclusive_scan(nullptr, tmpb, flag, vid, 0u, size_t(ntot) + 1,
-                                rocprim::plus<uint32_t>(), st));
-        tmp = ctx->buf("scan_tmp", tmpb);
-        LSM_HIP_TRY(ctx, rocprim::exclusive_scan(tmp, tmpb, flag, vid, 0u, size_t(ntot) + 1,
-                                rocprim::plus<uint32_t>(), st));
-        voxel_reduce<<<nb, PT_THREADS, 0, st>>>(k_out, v_out, vid, flag, ntot, *pts, ptc, d_geo,
-                                                cent, vkeys, vpts, vcloud);
+        // keys, stable radix sort, heads, their exclusive scan (voxel ids), per-voxel sums
+        auto chain = [&](auto *kin, auto *kout) -> int {
+            using KeyT = std::remove_pointer_t<decltype(kin)>;
+            voxel_keys<KeyT><<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, *pts, d_off, d_cnt,
+                                                                      d_geo, v, kin, v_in);
+            size_t tb = 0;
+            LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(nullptr, tb, kin, kout, v_in, v_out,
+                                                       size_t(ntot), 0, endbit, st));
+            void *tp = ctx->buf("sort_tmp", tb);
+            if (!tp) return LSM_ENOMEM;
+            LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(tp, tb, kin, kout, v_in, v_out, size_t(ntot),
+                                                       0, endbit, st));
+            voxel_flags<KeyT><<<nb, PT_THREADS, 0, st>>>(kout, ntot, flag);
+            LSM_HIP_TRY(ctx, hipMemsetAsync(flag + ntot, 0, 4, st));
+            tb = 0;
+            LSM_HIP_TRY(ctx, rocprim::exclusive_scan(nullptr, tb, flag, vid, 0u, size_t(ntot) + 1,
+                                                     rocprim::plus<uint32_t>(), st));
+            tp = ctx->buf("scan_tmp", tb);
+            if (!tp) return LSM_ENOMEM;
+            LSM_HIP_TRY(ctx, rocprim::exclusive_scan(tp, tb, flag, vid, 0u, size_t(ntot) + 1,
+                                                     rocprim::plus<uint32_t>(), st));
+            voxel_heads<<<nb, PT_THREADS, 0, st>>>(flag, vid, ntot, vstart);
+            voxel_reduce<KeyT><<<nb, PT_THREADS, 0, st>>>(kout, v_out, vid, vstart, ntot, *pts, ptc,
+                                                          d_geo, cent, vkeys, vpts, vcloud);
+            return LSM_OK;
+        };
+        rc = endbit <= 32 ? chain(reinterpret_cast<uint32_t *>(k_in), reinterpret_cast<uint32_t *>(k_out))
+                          : chain(k_in, k_out);
+        if (rc) return rc;
         // voxels per cloud: the sort keeps each cloud's keys together (key_off), so cloud k's
         // voxel ids run from vid[P_k] to vid[P_k+1], P_k = the points of the clouds before it
         std::vector<uint32_t> pstart(size_t(K) + 1, 0);
@@ -2052,7 +2142,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     if ((rc = upload_vec(ctx, "g_cnt", wn, &d_cn))) return rc;
     double *d_bb = (double *)ctx->buf("g_bb", size_t(K) * 48);
     if (!d_bb) return LSM_ENOMEM;
-    bbox_kernel<<<K, 256, 0, st>>>(wpts, d_coff, d_cn, d_bb);
+    if ((rc = run_bbox(ctx, wpts, d_coff, d_cn, K, d_bb, "g_bbk"))) return rc;
     std::vector<double> bb(size_t(K) * 6);
     LSM_HIP_TRY(ctx, hipMemcpyAsync(bb.data(), d_bb, bb.size() * 8, hipMemcpyDeviceToHost, st));
     LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
@@ -2408,11 +2498,41 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
             if (!d_ns) return LSM_ENOMEM;
             LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 72 * 8, st));
         }
+        // the eager path's split launch (sparse half, then the deferred points in full waves;
+        // bit-identical to the one-kernel form, points already computed are skipped) unless
+        // LSM_NORMALS_SPLIT=0 (read per call): one complete_normals_kernel over the pending points
+        const char *sp = getenv("LSM_NORMALS_SPLIT");
+        const bool split = !sp || atoi(sp) != 0;
+        GridGeo *d_gg = nullptr;
+        uint32_t *dlist = nullptr, *dcnt = nullptr;
+        if (split && !segs.empty()) {
+            std::vector<GridGeo> gg(grp.size());
+            uint32_t tot = 0;
+            for (size_t k = 0; k < grp.size(); ++k) {
+                gg[k] = GridGeo{};
+                gg[k].pt_off = tot;
+                gg[k].n = n[k];
+                tot += n[k];
+            }
+            if ((rc = upload_vec(ctx, "lz_gg", gg, &d_gg))) return rc;
+            dlist = (uint32_t *)ctx->buf("lz_dlist", size_t(tot) * 4);
+            dcnt = (uint32_t *)ctx->buf("lz_dcnt", grp.size() * 4);
+            if (!dlist || !dcnt) return LSM_ENOMEM;
+            LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, grp.size() * 4, st));
+        }
         hipEvent_t ev;
         ctx->tic("normals_lazy", &ev);
-        if (!segs.empty())
-            complete_normals_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(
-                d_segs, d_cd, normal_params(r, mnn), d_ns);
+        if (!segs.empty()) {
+            const NormalParams np = normal_params(r, mnn);
+            if (split) {
+                normals_sparse_kernel<2><<<int(segs.size()), PT_THREADS, 0, st>>>(
+                    d_segs, d_cd, d_gg, np, dlist, dcnt, d_ns);
+                normals_dense_kernel<2><<<int(segs.size()), PT_THREADS, 0, st>>>(
+                    d_segs, d_cd, d_gg, np, dlist, dcnt, d_ns);
+            } else {
+                complete_normals_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_ns);
+            }
+        }
         ctx->toc("normals_lazy", ev);
         LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
         LSM_HIP_TRY(ctx, hipGetLastError());
@@ -2422,7 +2542,14 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
             unsigned long long nbr = 0;
             for (int k = 8; k < 72; ++k) nbr += h[k];
             ctx->stats["normals_neighbours"].launches += int64_t(nbr);
-            ctx->stats["normals_points"].launches += int64_t(h[1]);
+            if (split) {   // (the split kernels count no points: the pending ones, all of them
+                           // unless an earlier per-point batch computed some)
+                int64_t np_ = 0;
+                for (uint32_t v : n) np_ += v;
+                ctx->stats["normals_points"].launches += np_;
+            } else {
+                ctx->stats["normals_points"].launches += int64_t(h[1]);
+            }
         }
         for (Cloud *c : grp) c->lazy = false;
         todo.swap(rest);
