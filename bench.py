@@ -300,15 +300,17 @@ def main():
         from lidar_slam_arvc_amd.multiscale import MultiScaleSet
         ms = MultiScaleSet(dev, ids)                 # per-scale device clones, made once
 
+        n_fine = []   # points per scan at the finest scale: the same every step, read once
+
         def step():
             ms.preprocess(want_normals=wn_mode, grid_cell=args.grid_cell)
             stages = ms.register(list(range(1, P + 1)), list(range(P)), seq.priors,
-                                 method=args.method)
+                                 method=args.method, arrays=True)
             res = stages[-1]
-            rel = np.stack([r["transformation"] for r in res])
-            compose_global_sharded(rel, group=group, device=cuda)
-            n = [dev.info(h)[1] for h in ms.handles[-1]]
-            return n, res
+            compose_global_sharded(res["transformation"], group=group, device=cuda)
+            if not n_fine:
+                n_fine.extend(dev.info(h)[1] for h in ms.handles[-1])
+            return n_fine, res
     elif loop:
         prep = _lib.prep_params(want_normals=wn_mode, grid_cell=args.grid_cell)
         icp = _lib.icp_params(method=args.method)

@@ -46,9 +46,10 @@ class MultiScaleSet:
                                                      **prep_kwargs))
 
     def register(self, src_idx, tgt_idx, inits=None, max_corr=DEFAULT_MAX_CORR,
-                 method="p2plane", max_iteration=30):
+                 method="p2plane", max_iteration=30, arrays=False):
         """Pairs (src_idx[k] onto tgt_idx[k], indices into raw_handles) through every scale.
-        Returns the per-stage lists of :meth:`Device.icp_batch` result dicts."""
+        Returns the per-stage lists of :meth:`Device.icp_batch` result dicts (``arrays``: the
+        per-stage dicts of arrays of :meth:`Device.icp_batch_arrays`, no per-pair objects)."""
         max_corr = tuple(float(d) for d in max_corr)
         if len(max_corr) != len(self.scales):
             raise ValueError("one max_correspondence_distance per scale")
@@ -61,12 +62,16 @@ class MultiScaleSet:
              else np.asarray(inits, dtype=np.float64).reshape(P, 4, 4).copy())
         stages = []
         for hs, dmax in zip(self.handles, max_corr):
-            res = self.dev.icp_batch([hs[i] for i in src_idx], [hs[i] for i in tgt_idx],
-                                     T.reshape(P, 16),
-                                     _lib.icp_params(method=method,
-                                                     max_correspondence_distance=dmax,
-                                                     max_iteration=max_iteration))
-            T = np.stack([r["transformation"] for r in res])
+            prm = _lib.icp_params(method=method, max_correspondence_distance=dmax,
+                                  max_iteration=max_iteration)
+            src = [hs[i] for i in src_idx]
+            tgt = [hs[i] for i in tgt_idx]
+            if arrays:
+                res = self.dev.icp_batch_arrays(src, tgt, T.reshape(P, 16), prm)
+                T = res["transformation"]
+            else:
+                res = self.dev.icp_batch(src, tgt, T.reshape(P, 16), prm)
+                T = np.stack([r["transformation"] for r in res])
             stages.append(res)
         return stages
 

@@ -1,14 +1,23 @@
 """Idle gaps of the GPU between consecutive kernels of a rocprofv3 kernel trace (host work the
-device waits for), summed by the kernel that precedes the gap, over the last N ms of the trace.
-python tools/gap_timeline.py run_kernel_trace.csv [window_ms]"""
+device waits for), summed by the kernel they precede, over the last N ms of the trace -- or, with
+a marker kernel name, over the window between its (2 per)-th- and per-th-last launches
+(one step of a bench run that ends with an untimed statistics step; per = marker launches per
+step). python tools/gap_timeline.py run_kernel_trace.csv[.gz] [window_ms | marker per]"""
 import csv
+import gzip
 import sys
 from collections import defaultdict
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-window = float(sys.argv[2]) * 1e6 if len(sys.argv) > 2 else None
+f = gzip.open(sys.argv[1], "rt") if sys.argv[1].endswith(".gz") else open(sys.argv[1])
+rows = list(csv.DictReader(f))
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
-if window is not None:
+if len(sys.argv) > 3:
+    marker, per = sys.argv[2], int(sys.argv[3])
+    starts = [s for s, _, n in ev if marker in n]
+    a, b = starts[-2 * per], starts[-per]
+    ev = [x for x in ev if a <= x[0] < b]
+elif len(sys.argv) > 2:
+    window = float(sys.argv[2]) * 1e6
     t_end = max(e for _, e, _ in ev)
     ev = [x for x in ev if x[0] >= t_end - window]
 
