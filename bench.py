@@ -51,7 +51,7 @@ def parse():
                          "ouster_multiscale: C5 256k Ouster-128, voxel 0.4/0.2/0.1 m chain; "
                          "loop_closure: C4 independent 64k revisit pairs (sharded, no halo)")
     ap.add_argument("--pairs-per-gpu", type=int, default=0,
-                    help="0: 1999 (hdl64: the C3 2000-keyframe sequence), 256 (ouster), "
+                    help="0: 1999 (hdl64: the C3 2000-keyframe sequence), 512 (ouster), "
                          "512 (loop_closure: C4's 4096 pairs over 8 GPUs)")
     ap.add_argument("--seed", type=int, default=-1, help="-1: 3 (hdl64), 5 (ouster)")
     ap.add_argument("--method", default="p2plane", choices=["p2plane", "p2p"])
@@ -246,7 +246,7 @@ def main():
     loop = args.workload == "loop_closure"
     if args.normals == "auto":
         args.normals = "lazy" if (ouster or loop) else "eager"
-    P = args.pairs_per_gpu or (256 if ouster else (512 if loop else 1999))
+    P = args.pairs_per_gpu or (512 if ouster else (512 if loop else 1999))
     first = rank * P
     model = synthetic.OUSTER128 if ouster else synthetic.HDL64
     seed = args.seed if args.seed >= 0 else (5 if ouster else (4 if loop else 3))

@@ -180,6 +180,24 @@ __global__ void bbox_final(const uint32_t *bbk, int K, double *bb) {
     bb[i] = (lo && k == 0xffffffffu) ? INFINITY : ((!lo && k == 0u) ? -INFINITY : double(key_f32(k)));
 }
 
+// per-cloud (off, cnt) of the filter's output from its block offsets (no host round trip)
+__global__ void filter_cloud_ranges(const uint32_t *boff, const int32_t *first_block,
+                                    const int32_t *nblocks, int K, uint32_t *off, uint32_t *cnt) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const int f = first_block[k], nb = nblocks[k];
+    off[k] = nb ? boff[f] : 0u;
+    cnt[k] = nb ? boff[f + nb] - boff[f] : 0u;
+}
+
+// per-cloud (off, cnt) of the voxel centroids from the clouds' first voxel ids vb[0 .. K]
+__global__ void vox_cloud_ranges(const uint32_t *vb, int K, uint32_t *off, uint32_t *cnt) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    off[k] = vb[k] - vb[0];
+    cnt[k] = vb[k + 1] - vb[k];
+}
+
 // bb[6 k .. 6 k + 6) = (min xyz, max xyz) of cloud k
 int run_bbox(lsm_ctx *ctx, const float4 *pts, const uint32_t *d_off, const uint32_t *d_cnt, int K,
              double *d_bb, const char *name) {
@@ -1878,8 +1896,11 @@ std::vector<Seg> point_segments(const std::vector<uint32_t> &n, int per_block) {
 
 // filter_radius_height over the batch: writes the kept points of cloud k, in reference order, to
 // out[off[k] .. off[k] + cnt[k]).
+// Also the boxes of the filtered clouds (bb: 6 per cloud), read back with the counts in one
+// synchronisation (the voxel grid or the spatial grid needs them next).
 int run_filter(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params &p,
-               float4 **out, std::vector<uint32_t> &off, std::vector<uint32_t> &cnt) {
+               float4 **out, std::vector<uint32_t> &off, std::vector<uint32_t> &cnt,
+               std::vector<double> &bb) {
     hipStream_t st = ctx->stream;
     const int K = int(clouds.size());
     std::vector<const float *> raw(K);
@@ -1937,9 +1958,27 @@ int run_filter(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params
         filter_write<<<nfb, FILTER_THREADS, 0, st>>>(d_fsegs, d_raw, d_nraw, fp, d_boff, d_fpts,
                                                      d_fidx);
         ctx->toc("filter", ev);
+        int32_t *d_fb, *d_nb;
+        uint32_t *d_off = (uint32_t *)ctx->buf("f_coff", size_t(K) * 4);
+        uint32_t *d_cnt = (uint32_t *)ctx->buf("f_ccnt", size_t(K) * 4);
+        double *d_bb = (double *)ctx->buf("f_bb", size_t(K) * 48);
+        if (!d_off || !d_cnt || !d_bb) return LSM_ENOMEM;
+        if ((rc = upload_vec(ctx, "f_fb", first_block, &d_fb))) return rc;
+        if ((rc = upload_vec(ctx, "f_nb", nblocks, &d_nb))) return rc;
+        filter_cloud_ranges<<<(K + 255) / 256, 256, 0, st>>>(d_boff, d_fb, d_nb, K, d_off, d_cnt);
+        if ((rc = run_bbox(ctx, d_fpts, d_off, d_cnt, K, d_bb, "f_bbk"))) return rc;
+        bb.resize(size_t(K) * 6);
         LSM_HIP_TRY(ctx, hipMemcpyAsync(boff_h.data(), d_boff, boff_h.size() * 4,
                                         hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(bb.data(), d_bb, bb.size() * 8, hipMemcpyDeviceToHost, st));
         LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    } else {
+        bb.assign(size_t(K) * 6, 0.0);
+        for (int k = 0; k < K; ++k)
+            for (int a = 0; a < 3; ++a) {   // empty clouds: (+inf, -inf), as bbox_final leaves them
+                bb[6 * k + a] = INFINITY;
+                bb[6 * k + 3 + a] = -INFINITY;
+            }
     }
     off.assign(K, 0);
     cnt.assign(K, 0);
@@ -1959,8 +1998,10 @@ int run_filter(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params
 
 // voxel_down_sample over the batch; replaces (pts, off, cnt) by the voxel centroids (f32 working
 // copy) and stores the f64 centroids / int32 keys on each cloud.
+// bb: the filtered clouds' boxes in, the voxelised clouds' boxes out (read back with the voxel
+// counts in one synchronisation)
 int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts,
-              std::vector<uint32_t> &off, std::vector<uint32_t> &cnt) {
+              std::vector<uint32_t> &off, std::vector<uint32_t> &cnt, std::vector<double> &bb) {
     hipStream_t st = ctx->stream;
     const int K = int(clouds.size());
     int rc;
@@ -1969,12 +2010,6 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
     uint32_t *d_off, *d_cnt;
     if ((rc = upload_vec(ctx, "v_off", off, &d_off))) return rc;
     if ((rc = upload_vec(ctx, "v_cnt", cnt, &d_cnt))) return rc;
-    double *d_bb = (double *)ctx->buf("v_bb", size_t(K) * 48);
-    if (!d_bb) return LSM_ENOMEM;
-    if ((rc = run_bbox(ctx, *pts, d_off, d_cnt, K, d_bb, "v_bbk"))) return rc;
-    std::vector<double> bb(size_t(K) * 6);
-    LSM_HIP_TRY(ctx, hipMemcpyAsync(bb.data(), d_bb, bb.size() * 8, hipMemcpyDeviceToHost, st));
-    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
     std::vector<VoxGeo> geo(K);
     uint64_t key_off = 0;
     for (int k = 0; k < K; ++k) {
@@ -2073,9 +2108,17 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
         if (!d_vb) return LSM_ENOMEM;
         if ((rc = upload_vec(ctx, "v_pstart", pstart, &d_pstart))) return rc;
         vox_cloud_bounds<<<(K + 1 + 255) / 256, 256, 0, st>>>(vid, d_pstart, K + 1, d_vb);
+        // the centroids' boxes for the spatial grid, before the one read-back
+        uint32_t *d_voff = (uint32_t *)ctx->buf("v_coff", size_t(K) * 4);
+        uint32_t *d_vcnt = (uint32_t *)ctx->buf("v_ccnt", size_t(K) * 4);
+        double *d_vbb = (double *)ctx->buf("v_bb", size_t(K) * 48);
+        if (!d_voff || !d_vcnt || !d_vbb) return LSM_ENOMEM;
+        vox_cloud_ranges<<<(K + 255) / 256, 256, 0, st>>>(d_vb, K, d_voff, d_vcnt);
+        if ((rc = run_bbox(ctx, vpts, d_voff, d_vcnt, K, d_vbb, "v_bbk"))) return rc;
         ctx->toc("voxel", ev);
         std::vector<uint32_t> vb(size_t(K) + 1);
         LSM_HIP_TRY(ctx, hipMemcpyAsync(vb.data(), d_vb, vb.size() * 4, hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(bb.data(), d_vbb, bb.size() * 8, hipMemcpyDeviceToHost, st));
         LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
         nvox = vb[K];
         for (int k = 0; k < K; ++k) vcount[k] = vb[k + 1] - vb[k];
@@ -2132,20 +2175,12 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     // ---------------- filter / voxel ----------------
     float4 *wpts = nullptr;
     std::vector<uint32_t> woff, wn;
-    if ((rc = run_filter(ctx, clouds, p, &wpts, woff, wn))) return rc;
+    std::vector<double> bb;   // boxes of the clouds the grid indexes (filtered, or voxelised)
+    if ((rc = run_filter(ctx, clouds, p, &wpts, woff, wn, bb))) return rc;
     const bool vox = p.voxel_size > 0.0;
-    if (vox && (rc = run_voxel(ctx, clouds, p.voxel_size, &wpts, woff, wn))) return rc;
+    if (vox && (rc = run_voxel(ctx, clouds, p.voxel_size, &wpts, woff, wn, bb))) return rc;
 
     // ---------------- spatial grid ----------------
-    uint32_t *d_coff, *d_cn;
-    if ((rc = upload_vec(ctx, "g_off", woff, &d_coff))) return rc;
-    if ((rc = upload_vec(ctx, "g_cnt", wn, &d_cn))) return rc;
-    double *d_bb = (double *)ctx->buf("g_bb", size_t(K) * 48);
-    if (!d_bb) return LSM_ENOMEM;
-    if ((rc = run_bbox(ctx, wpts, d_coff, d_cn, K, d_bb, "g_bbk"))) return rc;
-    std::vector<double> bb(size_t(K) * 6);
-    LSM_HIP_TRY(ctx, hipMemcpyAsync(bb.data(), d_bb, bb.size() * 8, hipMemcpyDeviceToHost, st));
-    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
 
     std::vector<GridGeo> geo(K);
     uint64_t cell_total = 0;
