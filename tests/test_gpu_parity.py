@@ -64,7 +64,7 @@ def test_filter_edges(dev):
 
 
 # ------------------------------------------------------------------ voxel (a3)
-@pytest.mark.parametrize("v", [0.1, 0.25, 0.4])
+@pytest.mark.parametrize("v", [0.01, 0.1, 0.25, 0.4])   # 0.01: a 64-bit key space
 def test_voxel_bit_exact(dev, seq8k, v):
     ids = _prep(dev, seq8k.scans[:2], want_normals=False, voxel_size=v)
     try:
