@@ -109,6 +109,7 @@ static void free_cloud(Cloud *c) {
     (void)hipFree(c->d_nrm);
     (void)hipFree(c->d_perm);
     (void)hipFree(c->d_cell);
+    (void)hipFree(c->d_bmask);
     (void)hipFree(c->d_vox);
     (void)hipFree(c->d_vkeys);
     (void)hipFree(c->d_prior_ref);

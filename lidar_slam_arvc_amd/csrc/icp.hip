@@ -908,6 +908,9 @@ __device__ __forceinline__ float gap2(float q, float lo, float hi) {
 __device__ __forceinline__ int ring_size(int r) { return r == 0 ? 1 : 24 * r * r + 2; }
 __device__ __forceinline__ int ring_prefix(int r) { return r == 0 ? 0 : (2 * r - 1) * (2 * r - 1) * (2 * r - 1); }
 constexpr int FB_R0 = 2;   // the fallback's first shell: rings 0 .. FB_R0 (5 x 5 x 5 blocks)
+#ifndef LSM_FB_BMASK
+#define LSM_FB_BMASK 1     // empty-block test from the block occupancy bits
+#endif
 // the first shell's block offsets (dx, dy, dz) centre-out, by |offset|^2: the blocks nearest the
 // query are scanned first, so the pruning radius shrinks before the outer blocks are tested
 __constant__ int8_t c_shell[3 * 125] = {
@@ -1057,8 +1060,15 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                             if (lb2 * 0.9999f < t2.lim) {
                                 lb = lb2;
                                 const int bid = (bz * G.nby + by) * G.nbx + bx;
-                                a = lsm_ld(cs, size_t(bid) * LSM_BLK_CELLS);
-                                b = lsm_ld(cs, size_t(bid + 1) * LSM_BLK_CELLS);
+#if LSM_FB_BMASK
+                                // empty blocks (most of a far query's rings) end at the
+                                // occupancy bit, an L1 hit, without the cell-table loads
+                                if ((lsm_ld(G.bmask, bid >> 5) >> (bid & 31)) & 1u)
+#endif
+                                {
+                                    a = lsm_ld(cs, size_t(bid) * LSM_BLK_CELLS);
+                                    b = lsm_ld(cs, size_t(bid + 1) * LSM_BLK_CELLS);
+                                }
                             }
                         }
                     }

@@ -24,6 +24,7 @@ struct CloudDev {
     const float4 *xyz;          // n, cell-sorted
     const float4 *nrm;          // n or nullptr
     const uint32_t *cell_start; // ncells + 1, offsets into xyz
+    const uint32_t *bmask;      // occupancy bit per 4x4x4 block (block id (bz*nby + by)*nbx + bx)
     float ox, oy, oz;           // grid origin
     float cell, inv_cell;       // cell edge and its reciprocal
     int nx, ny, nz;             // cells per axis

@@ -495,6 +495,29 @@ grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const
     }
 }
 
+// Block occupancy bits (bit b: block b's 64 cells hold a point), one wave per 64 blocks: the
+// correspondence fallback skips empty blocks without loading their cell-table entries.
+__global__ void __launch_bounds__(256)
+block_mask_kernel(const GridGeo *geo, int ncloud, uint32_t *const *cell_ptrs,
+                  uint32_t *const *bm_ptrs) {
+    const int c = blockIdx.y;
+    if (c >= ncloud) return;
+    const GridGeo G = geo[c];
+    const uint32_t nb = G.ncells / LSM_BLK_CELLS;
+    const uint32_t *cs = cell_ptrs[c];
+    uint32_t *bm = bm_ptrs[c];
+    for (uint32_t b0 = blockIdx.x * 256u; b0 < nb; b0 += gridDim.x * 256u) {
+        const uint32_t b = b0 + threadIdx.x;
+        const bool occ = b < nb && cs[size_t(b + 1) * LSM_BLK_CELLS] > cs[size_t(b) * LSM_BLK_CELLS];
+        const uint64_t m = __ballot(occ);
+        const uint32_t wb = b0 + (threadIdx.x & ~63u);   // this wave's first block
+        if ((threadIdx.x & 63) == 0 && wb < nb) {   // (2 words per 64 blocks are allocated)
+            bm[wb / 32] = uint32_t(m);
+            bm[wb / 32 + 1] = uint32_t(m >> 32);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // normals: KDTreeSearchParamHybrid(radius, max_nn) neighbourhoods on the cell grid
 // ------------------------------------------------------------------------------------------
@@ -2226,7 +2249,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         }
     }
     std::vector<CloudDev> cdev(K);
-    std::vector<uint32_t *> perm_ptrs(K), cell_ptrs(K);
+    std::vector<uint32_t *> perm_ptrs(K), cell_ptrs(K), bm_ptrs(K);
     for (int k = 0; k < K; ++k) {
         Cloud *c = clouds[k];
         if ((rc = ensure_cloud_buffers(ctx, c, wn[k], p.want_normals != 0))) return rc;
@@ -2249,8 +2272,19 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 return LSM_ENOMEM;
             }
         }
+        const int64_t bmw = ((ncells / LSM_BLK_CELLS + 63) / 64) * 2;
+        if (c->bmask_cap < bmw || !c->d_bmask) {
+            (void)hipFree(c->d_bmask);
+            c->d_bmask = nullptr;
+            c->bmask_cap = bmw;
+            if (hipMalloc(&c->d_bmask, size_t(bmw) * 4) != hipSuccess) {
+                ctx->set_error("hipMalloc failed (block mask)");
+                return LSM_ENOMEM;
+            }
+        }
         CloudDev &D = cdev[k];
         D.xyz = c->d_xyz;
+        D.bmask = c->d_bmask;
         D.nrm = p.want_normals ? c->d_nrm : nullptr;
         D.cell_start = c->d_cell;
         D.ox = geo[k].ox;
@@ -2270,10 +2304,12 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                           ? c->d_prior_ref : nullptr;
         perm_ptrs[k] = c->d_perm;
         cell_ptrs[k] = c->d_cell;
+        bm_ptrs[k] = c->d_bmask;
     }
     GridGeo *d_geo;
     CloudDev *d_cd;
-    uint32_t **d_perm_ptrs, **d_cell_ptrs;
+    uint32_t **d_perm_ptrs, **d_cell_ptrs, **d_bm_ptrs;
+    if ((rc = upload_vec(ctx, "g_bmp", bm_ptrs, &d_bm_ptrs))) return rc;
     if ((rc = upload_vec(ctx, "g_geo", geo, &d_geo))) return rc;
     if ((rc = upload_vec(ctx, "g_cd", cdev, &d_cd))) return rc;
     if ((rc = upload_vec(ctx, "g_perm", perm_ptrs, &d_perm_ptrs))) return rc;
@@ -2311,6 +2347,8 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     {
         const int gx = int(std::min<int64_t>((maxcells1 + FILL_TILE - 1) / FILL_TILE, 4096));
         grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs);
+        const int bx = int(std::min<int64_t>((maxcells1 / LSM_BLK_CELLS + 255) / 256, 1024));
+        block_mask_kernel<<<dim3(std::max(bx, 1), K), 256, 0, st>>>(d_geo, K, d_cell_ptrs, d_bm_ptrs);
     }
     ctx->toc("grid", ev);
 
