@@ -1008,7 +1008,15 @@ struct NPhase {
 //   NL_COOP:   NL_DENSE with scan 1 and the final pass run cooperatively by the wave
 //              (coop_visit); every lane of the wave must call it (`act` false: no point).
 // Returns false when the point was deferred.
-constexpr int NL_AUTO = 0, NL_SPARSE = 1, NL_DENSE = 2, NL_COOP = 3;
+//   NL_DENSE_NR: NL_DENSE without the refine scans: a point that needs one (a saturated u8 bin, or
+//              a chosen bin holding more than SEL_CAP members: 0.002 % of the dense points) is
+//              deferred (returns false) to normals_refine_kernel, which runs it as NL_DENSE. The
+//              refine scans' live state sets the dense kernel's register count (101 VGPRs, 93
+//              without them): leaving them out lets the dense half run 5 waves per SIMD.
+constexpr int NL_AUTO = 0, NL_SPARSE = 1, NL_DENSE = 2, NL_COOP = 3, NL_DENSE_NR = 4;
+#ifndef LSM_NSPARSE_BAND_DEFER
+#define LSM_NSPARSE_BAND_DEFER 1
+#endif
 #ifndef LSM_NDIAG
 #define LSM_NDIAG 0   // diagnostics builds only (wrong normals): 1 / 3 stop the dense half after
                       // scan 1 (3: without its histogram adds), 2 before its final pass
@@ -1128,7 +1136,7 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     const NormalsPts pts = normals_pts(C);
     // Dense-predicted points skip acc.add in scan 1 (histogram only); a wrong guess costs one
     // plain rescan below, which visits the ball in scan 1's order (identical sums).
-    const bool dense = (MODE == NL_DENSE || MODE == NL_COOP) ? true : predict_dense(C, np, qf);
+    const bool dense = (MODE == NL_DENSE || MODE == NL_COOP || MODE == NL_DENSE_NR) ? true : predict_dense(C, np, qf);
     if (MODE == NL_SPARSE && dense) return false;
     NP_ST(ph, 7, dense ? 1u : 0u);
     if (MODE != NL_SPARSE) {
@@ -1137,6 +1145,7 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     }
     Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
     bool sat = false;
+    bool band = false;   // NL_SPARSE: a rounding-band point was met (LSM_NSPARSE_BAND_DEFER)
     int count = 0;
     // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
     // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
@@ -1148,11 +1157,23 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
             const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
             const float f = dx * dx + dy * dy + dz * dz;
             if (MODE == NL_SPARSE) {   // the same ball membership as the binned test below
+#if LSM_NSPARSE_BAND_DEFER
+                // a point in the sphere's rounding band (exact f64 test) defers the lane to the
+                // dense half, which decides it exactly: the sparse kernel keeps no f64 distance
+                // code (registers) for a case of ~1e-3 of its lanes
+                if (in && f < np.r2_lo) {
+                    acc.add(p, k);
+                    ++count;
+                } else if (in && f <= np.r2_hi) {
+                    band = true;
+                }
+#else
                 if (in && (f < np.r2_lo ||
                            (f <= np.r2_hi && make_off(p, qx, qy, qz).d2 < np.r2))) {
                     acc.add(p, k);
                     ++count;
                 }
+#endif
                 return;
             }
             const float t = f * np.hscale;
@@ -1185,7 +1206,7 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         });
     }
     if (MODE == NL_SPARSE) {
-        if (count > np.max_nn) return false;
+        if (count > np.max_nn || band) return false;
         acc.finish();
         return true;
     }
@@ -1245,6 +1266,7 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         });
     };
     bool u8 = true;
+    if (MODE == NL_DENSE_NR && count > np.max_nn && sat) return false;   // refine: deferred
     if (count > np.max_nn && sat) {                             // a u8 bin saturated: level 0 as 32 x u32 bins
         Sel next = S;
         next.scale = double(NB32) / np.r2;
@@ -1274,6 +1296,7 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         S.b = bstar;
         if (!S.by_idx) top = fmin(top, S.lo + double(bstar + 1) / S.scale);
         if (bin_count <= SEL_CAP) break;
+        if (MODE == NL_DENSE_NR) return false;   // refine: deferred
         // next level over the chosen bin's range, clipped to the exact member extremes known
         // so far (so no member falls below lo: a clamped lowest bin could never split); the
         // extremes found by the same scan then replace the whole classification chain
@@ -1540,22 +1563,92 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
 // Split launch, second half: one lane per entry of the clouds' dense lists (NL_DENSE), so the
 // truncated neighbourhoods run in full waves. The grid is the first half's (a cloud's list never
 // holds more entries than the cloud has points); workgroups past the list return at once.
+#ifndef LSM_NORMALS_DEFER_REFINE
+#define LSM_NORMALS_DEFER_REFINE 1
+#endif
+// LSM_NDENSE_WPE: waves per SIMD requested for the dense half (0: no request)
+#ifndef LSM_NDENSE_WPE
+#define LSM_NDENSE_WPE 0
+#endif
+#if LSM_NDENSE_WPE > 0
+#define LSM_NDENSE_ATTR __attribute__((amdgpu_waves_per_eu(LSM_NDENSE_WPE)))
+#else
+#define LSM_NDENSE_ATTR LSM_NORMALS_ATTR
+#endif
 template <int G>
-__global__ void __launch_bounds__(PT_THREADS) LSM_NORMALS_ATTR
+__global__ void __launch_bounds__(PT_THREADS) LSM_NDENSE_ATTR
 normals_dense_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
-                     const uint32_t *dlist, const uint32_t *dcnt, unsigned long long *stats) {
+                     const uint32_t *dlist, const uint32_t *dcnt, unsigned long long *stats,
+                     uint32_t *rlist, uint32_t *rcnt) {
     __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
     const Seg s = segs[blockIdx.x];
     const uint32_t slot = uint32_t(s.start) + threadIdx.x;
     if (slot >= dcnt[s.cloud]) return;
     const CloudDev C = cd[s.cloud];
-    const int j = int(dlist[geo[s.cloud].pt_off + slot]);
+    const uint32_t off = geo[s.cloud].pt_off;
+    const int j = int(dlist[off + slot]);
     const float4 q = lsm_ld(C.xyz, j);
     CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
+#if LSM_NORMALS_DEFER_REFINE
+    // the rare points that need a refine scan go to the cloud's refine list
+    const bool done = hybrid_lane<G, CumAcc, false, NL_DENSE_NR, LSM_NORMALS_PFD>(
+        C, j, np, stats, lds + threadIdx.x * HSTRIDE, acc);
+    const uint64_t bm = __ballot(!done);
+    if (bm) {
+        const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)bm) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(rcnt + s.cloud, uint32_t(__popcll(bm)));
+        base = uint32_t(__shfl(int(base), leader, LSM_WAVE));
+        if (!done) rlist[off + base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = uint32_t(j);
+    }
+    if (stats && done) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+#else
+    (void)rlist;
+    (void)rcnt;
     hybrid_lane<G, CumAcc, false, NL_DENSE, LSM_NORMALS_PFD>(C, j, np, stats,
                                                              lds + threadIdx.x * HSTRIDE, acc);
     if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+#endif
+}
+
+// The dense half's deferred points (NL_DENSE with its refine scans): blockIdx.x = cloud, the
+// workgroups of a cloud stride over its refine list (most clouds have none).
+constexpr int REFINE_BLOCKS = 4;
+template <int G>
+__global__ void __launch_bounds__(PT_THREADS)
+normals_refine_kernel(const CloudDev *cd, const GridGeo *geo, NormalParams np,
+                      const uint32_t *rlist, const uint32_t *rcnt, unsigned long long *stats) {
+    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+    const int c = blockIdx.x;
+    const uint32_t n = rcnt[c];
+    const CloudDev C = cd[c];
+    const uint32_t off = geo[c].pt_off;
+    for (uint32_t slot = blockIdx.y * PT_THREADS + threadIdx.x; slot < n;
+         slot += gridDim.y * PT_THREADS) {
+        const int j = int(rlist[off + slot]);
+        const float4 q = lsm_ld(C.xyz, j);
+        CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
+                   C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
+        hybrid_lane<G, CumAcc, false, NL_DENSE, LSM_NORMALS_PFD>(C, j, np, stats,
+                                                                 lds + threadIdx.x * HSTRIDE, acc);
+        if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+    }
+}
+
+// The dense half of the split launch: the dense lists' points, then the few the dense kernel
+// deferred to a refine scan. rlist / rcnt: scratch of the dense lists' size / K words.
+template <int G>
+void launch_dense_half(hipStream_t st, const Seg *d_segs, int nseg, const CloudDev *d_cd,
+                       const GridGeo *d_geo, int K, const NormalParams &np, const uint32_t *dlist,
+                       const uint32_t *dcnt, unsigned long long *d_ns, uint32_t *rlist,
+                       uint32_t *rcnt, size_t xlds) {
+    normals_dense_kernel<G><<<nseg, PT_THREADS, xlds, st>>>(d_segs, d_cd, d_geo, np, dlist, dcnt,
+                                                            d_ns, rlist, rcnt);
+#if LSM_NORMALS_DEFER_REFINE
+    normals_refine_kernel<G><<<dim3(K, REFINE_BLOCKS), PT_THREADS, 0, st>>>(d_cd, d_geo, np, rlist,
+                                                                           rcnt, d_ns);
+#endif
 }
 
 // normals_dense_kernel with the scans run cooperatively by each wave (NL_COOP, coop_visit):
@@ -2406,9 +2499,11 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
             const bool split = !sp || atoi(sp) != 0;
             if (split) {
                 uint32_t *dlist = (uint32_t *)ctx->buf("n_dlist", N * 4);
-                uint32_t *dcnt = (uint32_t *)ctx->buf("n_dcnt", size_t(K) * 4);
-                if (!dlist || !dcnt) return LSM_ENOMEM;
-                LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, size_t(K) * 4, st));
+                uint32_t *dcnt = (uint32_t *)ctx->buf("n_dcnt", size_t(K) * 8);
+                uint32_t *rlist = (uint32_t *)ctx->buf("n_rlist", N * 4);
+                if (!dlist || !dcnt || !rlist) return LSM_ENOMEM;
+                uint32_t *rcnt = dcnt + K;   // the refine lists' counts
+                LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, size_t(K) * 8, st));
                 // LSM_NORMALS_GD: points per load group of the dense half (its occupancy is
                 // set by the LDS rows, so it has registers to spare for wider groups)
                 static const int GD = [] {
@@ -2432,13 +2527,13 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 if (coop)
                     normals_dense_coop_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
                 else if (GD == 8)
-                    normals_dense_kernel<8><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                    launch_dense_half<8>(st, d_psegs, int(psegs.size()), d_cd, d_geo, K, np, dlist, dcnt, d_ns, rlist, rcnt, xlds);
                 else if (GD == 4)
-                    normals_dense_kernel<4><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                    launch_dense_half<4>(st, d_psegs, int(psegs.size()), d_cd, d_geo, K, np, dlist, dcnt, d_ns, rlist, rcnt, xlds);
                 else if (GD == 3)
-                    normals_dense_kernel<3><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                    launch_dense_half<3>(st, d_psegs, int(psegs.size()), d_cd, d_geo, K, np, dlist, dcnt, d_ns, rlist, rcnt, xlds);
                 else
-                    normals_dense_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
+                    launch_dense_half<2>(st, d_psegs, int(psegs.size()), d_cd, d_geo, K, np, dlist, dcnt, d_ns, rlist, rcnt, xlds);
             } else if (G == 1) normals_kernel<1><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
             else if (G == 2) normals_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
             else if (G == 8) normals_kernel<8><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
@@ -2577,7 +2672,7 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
         const char *sp = getenv("LSM_NORMALS_SPLIT");
         const bool split = !sp || atoi(sp) != 0;
         GridGeo *d_gg = nullptr;
-        uint32_t *dlist = nullptr, *dcnt = nullptr;
+        uint32_t *dlist = nullptr, *dcnt = nullptr, *rlist = nullptr;
         if (split && !segs.empty()) {
             std::vector<GridGeo> gg(grp.size());
             uint32_t tot = 0;
@@ -2589,9 +2684,10 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
             }
             if ((rc = upload_vec(ctx, "lz_gg", gg, &d_gg))) return rc;
             dlist = (uint32_t *)ctx->buf("lz_dlist", size_t(tot) * 4);
-            dcnt = (uint32_t *)ctx->buf("lz_dcnt", grp.size() * 4);
-            if (!dlist || !dcnt) return LSM_ENOMEM;
-            LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, grp.size() * 4, st));
+            dcnt = (uint32_t *)ctx->buf("lz_dcnt", grp.size() * 8);
+            rlist = (uint32_t *)ctx->buf("lz_rlist", size_t(tot) * 4);
+            if (!dlist || !dcnt || !rlist) return LSM_ENOMEM;
+            LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, grp.size() * 8, st));
         }
         hipEvent_t ev;
         ctx->tic("normals_lazy", &ev);
@@ -2600,8 +2696,8 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
             if (split) {
                 normals_sparse_kernel<2><<<int(segs.size()), PT_THREADS, 0, st>>>(
                     d_segs, d_cd, d_gg, np, dlist, dcnt, d_ns);
-                normals_dense_kernel<2><<<int(segs.size()), PT_THREADS, 0, st>>>(
-                    d_segs, d_cd, d_gg, np, dlist, dcnt, d_ns);
+                launch_dense_half<2>(st, d_segs, int(segs.size()), d_cd, d_gg, int(grp.size()), np,
+                                     dlist, dcnt, d_ns, rlist, dcnt + grp.size(), 0);
             } else {
                 complete_normals_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_ns);
             }
