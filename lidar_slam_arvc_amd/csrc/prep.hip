@@ -1014,9 +1014,6 @@ struct NPhase {
 //              refine scans' live state sets the dense kernel's register count (101 VGPRs, 93
 //              without them): leaving them out lets the dense half run 5 waves per SIMD.
 constexpr int NL_AUTO = 0, NL_SPARSE = 1, NL_DENSE = 2, NL_COOP = 3, NL_DENSE_NR = 4;
-#ifndef LSM_NSPARSE_BAND_DEFER
-#define LSM_NSPARSE_BAND_DEFER 1
-#endif
 #ifndef LSM_NDIAG
 #define LSM_NDIAG 0   // diagnostics builds only (wrong normals): 1 / 3 stop the dense half after
                       // scan 1 (3: without its histogram adds), 2 before its final pass
@@ -1145,7 +1142,6 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     }
     Sel S = {-INFINITY, INFINITY, 0u, 0xffffffffu, 0.0, double(NB8) / np.r2, NB8, 0, 0};
     bool sat = false;
-    bool band = false;   // NL_SPARSE: a rounding-band point was met (LSM_NSPARSE_BAND_DEFER)
     int count = 0;
     // Scan 1 with f32 decisions: a point is certainly inside when f < r2_lo, and certainly in level-0 bin
     // floor(t) when t = f * hscale is more than 2e-4 from a bin edge (|t - t_exact| < 6e-5:
@@ -1157,23 +1153,11 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
             const float dx = p.x - qf.x, dy = p.y - qf.y, dz = p.z - qf.z;
             const float f = dx * dx + dy * dy + dz * dz;
             if (MODE == NL_SPARSE) {   // the same ball membership as the binned test below
-#if LSM_NSPARSE_BAND_DEFER
-                // a point in the sphere's rounding band (exact f64 test) defers the lane to the
-                // dense half, which decides it exactly: the sparse kernel keeps no f64 distance
-                // code (registers) for a case of ~1e-3 of its lanes
-                if (in && f < np.r2_lo) {
-                    acc.add(p, k);
-                    ++count;
-                } else if (in && f <= np.r2_hi) {
-                    band = true;
-                }
-#else
                 if (in && (f < np.r2_lo ||
                            (f <= np.r2_hi && make_off(p, qx, qy, qz).d2 < np.r2))) {
                     acc.add(p, k);
                     ++count;
                 }
-#endif
                 return;
             }
             const float t = f * np.hscale;
@@ -1206,7 +1190,7 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         });
     }
     if (MODE == NL_SPARSE) {
-        if (count > np.max_nn || band) return false;
+        if (count > np.max_nn) return false;
         acc.finish();
         return true;
     }
