@@ -770,8 +770,12 @@ __device__ __forceinline__ void flush_stats(const NNStat &ls, unsigned long long
 #ifndef LSM_NN_WPE
 #define LSM_NN_WPE 8
 #endif
-#if LSM_NN_WPE > 0
-#define LSM_NN_ATTR __attribute__((amdgpu_waves_per_eu(LSM_NN_WPE)))
+// LSM_NN_WPE0: the same request for the passes without the stability check (0, 1)
+#ifndef LSM_NN_WPE0
+#define LSM_NN_WPE0 LSM_NN_WPE
+#endif
+#if LSM_NN_WPE > 0 && LSM_NN_WPE0 > 0
+#define LSM_NN_ATTR __attribute__((amdgpu_waves_per_eu(CHECK ? LSM_NN_WPE : LSM_NN_WPE0)))
 #else
 #define LSM_NN_ATTR
 #endif
