@@ -26,7 +26,7 @@ nsteps = (bench["steps"] + bench["warmup"] + 1) if bench else 1
 
 
 def kname(n):
-    m = re.search(r"normals_(sparse_kernel|dense_kernel|dense_coop_kernel|kernel)", n)
+    m = re.search(r"normals_(sparse_kernel|dense_kernel|dense_coop_kernel|refine_kernel|kernel)", n)
     return m.group(0) if m else n
 
 
@@ -55,7 +55,7 @@ for k, v in per.items():
 tot = sum(d.get("SQ_INSTS_VALU", 0.0) for d in kern.values())
 mode = bench["config"]["normals"].split(", ")[-1] if bench else None
 print(json.dumps({
-    "kernel": "every normals launch of a step (split launch: normals_sparse_kernel + "
+    "kernel": "every normals launch of a step (split launch: normals_sparse_kernel + normals_refine_kernel + "
               "normals_dense_kernel; eager)",
     "source": "rocprofv3 --kernel-trace --pmc SQ_* (two passes of 8), bench.py --steps 2 "
               "--warmup 1, default workload (tools/pmc_normals_bench.sh)",
