@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round-3 (continued) GPU session: grid A/B (radix vs counting sort), the counting-sort kernels'
 # rocprof stats, and the C5 (Ouster multi-scale) timeline gaps (host-side idle).
+# (the normals diagnostics at the end expect lidar_slam_arvc_amd/_lib/ab/ndiag{1,2,3}.so built by
+#  tools/build_ab.sh NAME -DLSM_NDIAG=N; the grid A/B needs a build with LSM_GRID_RADIX, since removed)
 # usage: bash tools/gpu_r03c.sh TAG
 set -u
 TAG=${1:-run}
