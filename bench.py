@@ -411,11 +411,11 @@ def main():
         # statistics mode (every rank runs it: the step's collectives need all ranks)
         d0 = devs[0]
         d0.reset_stats()
-        os.environ["LSM_NORMALS_STATS"] = "1"
+        d0.set_timing(True, statistics=True)
         try:
             step()
         finally:
-            del os.environ["LSM_NORMALS_STATS"]
+            d0.set_timing(False)
         nb = d0.kernel_stats("normals_neighbours")["launches"]
         npts = d0.kernel_stats("normals_points")["launches"]
         step_s = norm_ms / args.steps * 1e-3

@@ -221,7 +221,9 @@ int lsm_se3_prefix(const double *rel, int64_t n, double *out);
  * With timing on, the library brackets every launch of the named kernel with HIP events on its
  * own stream and accumulates the durations. Kernel names: "nn" (correspondence search),
  * "nn_fallback", "accumulate", "solve", "normals", "normals_overflow", "filter", "grid".
- * algo_bytes: algorithmic bytes the kernel moved (SURVEY.md §8d model; nn only). */
+ * algo_bytes: algorithmic bytes the kernel moved (SURVEY.md §8d model; nn only).
+ * enable = 2 (statistics mode, slower): also count the neighbours of every normal computed
+ * ("normals_neighbours", "normals_points" and "normals_truncated" in `launches`). */
 int lsm_set_timing(lsm_ctx *ctx, int32_t enable);
 int lsm_kernel_stats(lsm_ctx *ctx, const char *kernel, int64_t *launches, double *total_ms,
                      double *algo_bytes);

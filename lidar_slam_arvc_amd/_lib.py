@@ -389,8 +389,11 @@ class Device:
         return part[:len(c)].copy()
 
     # -- instrumentation ---------------------------------------------------------------------
-    def set_timing(self, on: bool):
-        self.check(self.lib.lsm_set_timing(self.handle, 1 if on else 0), "lsm_set_timing")
+    def set_timing(self, on: bool, statistics: bool = False):
+        """Per-kernel event timing; statistics=True also counts the neighbours of every normal
+        computed (slower: statistics runs only)."""
+        level = 2 if statistics else (1 if on else 0)
+        self.check(self.lib.lsm_set_timing(self.handle, level), "lsm_set_timing")
 
     def kernel_stats(self, name: str):
         n, ms, b = C.c_int64(), C.c_double(), C.c_double()

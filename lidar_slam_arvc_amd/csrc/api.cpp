@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -13,6 +14,22 @@
 #include "lsm_ctx.h"
 
 static const char *kVersion = "liblidarsm 0.1 (gfx950)";
+
+// Test knobs: the search-path variants the GPU tests switch (through the environment, read per
+// call) to prove every path exact; the defaults are the shipped values. DESIGN.md §7 lists them
+// with the tests that cover each. No other environment variable changes the library's results
+// (diagnostics builds, -DLSM_DIAG, add statistics printers).
+static const char *const kKnobs[] = {
+    "LSM_NN_SPLIT",  "LSM_NN_SPLIT_PLACE", "LSM_NN_NOCERT", "LSM_NN_CERT_FROM",  "LSM_NN_DIRECT",
+    "LSM_NN_DIRECT_ITER", "LSM_NN_KCOLD", "LSM_NN_KMAX",   "LSM_NORMALS_EXACT", "LSM_NORMALS_SPLIT"};
+
+double lsm_knob(const char *name, double dflt) {
+    bool known = false;
+    for (const char *k : kKnobs) known = known || std::strcmp(k, name) == 0;
+    if (!known) return dflt;
+    const char *e = std::getenv(name);
+    return e && *e ? std::atof(e) : dflt;
+}
 
 // ------------------------------------------------------------------------------------------
 // lsm_ctx helpers
@@ -114,7 +131,6 @@ static void free_cloud(Cloud *c) {
     (void)hipFree(c->d_vkeys);
     (void)hipFree(c->d_prior_ref);
     (void)hipFree(c->d_fpfh);
-    (void)hipFree(c->d_nstate);
     delete c;
 }
 
@@ -724,6 +740,7 @@ int lsm_loop_triplet_partners(lsm_ctx *ctx, const double *positions, int64_t m,
 int lsm_set_timing(lsm_ctx *ctx, int32_t enable) {
     if (!ctx) return LSM_EINVAL;
     ctx->timing = enable != 0;
+    ctx->statistics = enable >= 2;
     return LSM_OK;
 }
 

@@ -12,9 +12,13 @@ struct d3 {
 };
 
 __device__ __forceinline__ d3 d3_cross(d3 a, d3 b) {
+#pragma clang fp contract(off)
     return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-__device__ __forceinline__ double d3_dot(d3 a, d3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ double d3_dot(d3 a, d3 b) {
+#pragma clang fp contract(off)
+    return (a.x * b.x + a.y * b.y) + a.z * b.z;
+}
 
 // Symmetric matrix kept as its 6 unique entries.
 struct sym3 {
@@ -22,6 +26,7 @@ struct sym3 {
 };
 
 __device__ __forceinline__ d3 fe_vec0(const sym3 &A, double e) {
+#pragma clang fp contract(off)
     d3 r0 = {A.a00 - e, A.a01, A.a02};
     d3 r1 = {A.a01, A.a11 - e, A.a12};
     d3 r2 = {A.a02, A.a12, A.a22 - e};
@@ -47,6 +52,7 @@ __device__ __forceinline__ d3 fe_vec0(const sym3 &A, double e) {
 }
 
 __device__ __forceinline__ d3 fe_vec1(const sym3 &A, d3 v0, double e) {
+#pragma clang fp contract(off)
     d3 U;
     if (fabs(v0.x) > fabs(v0.y)) {
         double il = 1.0 / sqrt(v0.x * v0.x + v0.z * v0.z);
@@ -95,6 +101,7 @@ __device__ __forceinline__ d3 fe_vec1(const sym3 &A, d3 v0, double e) {
 }
 
 __device__ inline d3 fast_eigen3x3_min(sym3 A) {
+#pragma clang fp contract(off)
     double mc = fmax(fmax(fmax(A.a00, A.a01), fmax(A.a02, A.a11)), fmax(A.a12, A.a22));
     if (mc == 0.0) return {0.0, 0.0, 0.0};
     A.a00 /= mc;

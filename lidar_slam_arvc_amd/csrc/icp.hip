@@ -74,17 +74,6 @@ struct FallbackItem {
     float margin;     // rho margin of this query (see prune2)
 };
 
-// Lazy normals (LSM_NORMALS_LAZY targets of a P2Plane batch): a correspondence to target point t
-// whose normal is still pending marks it needed, and flags its 256-point block, so that the
-// pass's normals step (lsm_normals_lazy_pass) computes it before accumulate reads it. Plain byte
-// stores: racing markers write the same values.
-__device__ __forceinline__ void lazy_mark(const CloudDev &G, int t, uint8_t *blkflag) {
-    if (G.nstate && t >= 0 && G.nstate[t] == 0) {
-        G.nstate[t] = 1;
-        blkflag[G.lazy_blk0 + (t >> 8)] = 1;
-    }
-}
-
 __device__ __forceinline__ bool better(float d2, int idx, float bd2, int bidx) {
     return d2 < bd2 || (d2 == bd2 && idx < bidx);
 }
@@ -694,7 +683,7 @@ __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &
                                            const CloudDev &G, int i, int64_t g,
                                            const NNParams &prm, int32_t *__restrict__ corr,
                                            int32_t *__restrict__ alt, float4 *__restrict__ cert,
-                                           float &m, uint8_t *blkflag) {
+                                           float &m) {
     const float4 s = lsm_ld(S.xyz, i);
     double x, y, z;
     transform_point(P.T, s, x, y, z);
@@ -731,7 +720,6 @@ __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &
             } else if (swap) {
                 corr[g] = sec;
                 alt[g] = prev;
-                lazy_mark(G, sec, blkflag);
             }
             return true;
         }
@@ -785,7 +773,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
           NNParams prm, int32_t *__restrict__ corr, int32_t *__restrict__ alt,
           float4 *__restrict__ cert, FallbackItem *__restrict__ queue,
           uint32_t *__restrict__ queue_n, uint32_t queue_cap, uint32_t *__restrict__ searched,
-          uint8_t *__restrict__ blkflag, unsigned long long *__restrict__ stats = nullptr) {
+          unsigned long long *__restrict__ stats = nullptr) {
     NNStat ls{};
     NNStat *ns = STATS ? &ls : nullptr;
     // one task per workgroup: the host sizes the grid from an earlier pass's plan, which only
@@ -808,7 +796,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         __shared__ float s_m[NN_THREADS];
         __shared__ int32_t s_cnt[NN_THREADS / LSM_WAVE];
         bool need = false;
-        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, alt, cert, m, blkflag);
+        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, alt, cert, m);
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         const uint64_t bm = __ballot(need);
         if (lane == 0) s_cnt[w] = __popcll(bm);
@@ -865,10 +853,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         if (lead) {
             corr[g] = pending ? -2 : result;
             alt[g] = pending ? -1 : a2;
-            if (!pending) {
-                cert[g] = make_float4(qp.x, qp.y, qp.z, r);
-                lazy_mark(G, result, blkflag);
-            }
+            if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
         }
         if (STATS) {
             if (sub != 0) ls.v[0] = 0;   // one search per query
@@ -892,10 +877,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
     if (live) {
         corr[g] = pending ? -2 : result;
         alt[g] = pending ? -1 : a2;
-        if (!pending) {
-            cert[g] = make_float4(qp.x, qp.y, qp.z, r);
-            lazy_mark(G, result, blkflag);
-        }
+        if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
     }
     if (STATS) flush_stats(ls, stats);
 }
@@ -995,8 +977,7 @@ __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
               const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
               uint32_t queue_cap, int32_t *__restrict__ corr, float4 *__restrict__ cert,
-              unsigned long long *__restrict__ fstats, float far2, int far,
-              uint8_t *__restrict__ blkflag) {
+              unsigned long long *__restrict__ fstats, float far2, int far) {
     // far = 0: the items whose box-search best is within sqrt(far2) (or all when far2 = inf);
     // far = 1: the others (expected to need wider rings: more lanes per query)
     constexpr int NG = LSM_WAVE / GL;
@@ -1145,7 +1126,6 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
             fs[5] += hit ? 1 : 0;
             corr[g] = hit ? t2.bidx : -1;
             cert[g] = make_float4(qx, qy, qz, hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound));
-            if (hit) lazy_mark(G, t2.bidx, blkflag);
         }
     }
     if (fstats && sub == 0)
@@ -1508,55 +1488,19 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
     }
     std::vector<CloudDev> cdev(uniq.size());
-    for (size_t k = 0; k < uniq.size(); ++k) {
-        cdev[k] = uniq[k]->dev;
-        cdev[k].nstate = nullptr;
-        cdev[k].lazy_blk0 = 0;
-    }
-    // lazy-normal targets of a P2Plane batch (LSM_NORMALS_LAZY). Default: every pending normal
-    // of a target is computed before the first pass, in one launch of full, cell-ordered
-    // workgroups -- the clouds that are never a P2Plane target (the sources of loop-closure or
-    // multi-scale batches) never compute theirs. LSM_NORMALS_LAZY_POINTS=1 (read per call)
-    // computes, pass by pass, only the normals the correspondences reach: bit-identical, but
-    // slower on the 1999-pair sequence (41 vs 23 ms of normals per 256 pairs: the needed points
-    // are 76 % of the targets', yet their compacted waves run 1.4-2x the eager cost per wave,
-    // and each of the ~10 tail passes waits ~1 ms on a handful of dense-point waves, DESIGN.md
-    // §7). One (radius, max_nn) per batch: targets pending with other parameters are completed.
-    LazyNormals lz;
-    std::vector<int32_t> tb_off, lazy_cd;
-    std::vector<int64_t> pt_off;
+    for (size_t k = 0; k < uniq.size(); ++k) cdev[k] = uniq[k]->dev;
+    // lazy-normal targets of a P2Plane batch (LSM_NORMALS_LAZY): every pending normal of a
+    // target is computed before the first pass, in one launch of full, cell-ordered workgroups,
+    // so the clouds that are never a P2Plane target (the sources of loop-closure or multi-scale
+    // batches) never compute theirs. (Computing, pass by pass, only the normals the
+    // correspondences reach was bit-identical but slower: DESIGN.md §7.)
     if (p.method == LSM_P2PLANE) {
         std::vector<char> is_tgt(uniq.size(), 0);
         for (int64_t k = 0; k < npairs; ++k) is_tgt[size_t(ti[k])] = 1;
-        const char *lp = getenv("LSM_NORMALS_LAZY_POINTS");
-        const bool per_point = lp && atoi(lp) != 0;
-        std::vector<Cloud *> other;
-        for (size_t k = 0; k < uniq.size(); ++k) {
-            Cloud *c = uniq[k];
-            if (!is_tgt[k] || !c->lazy) continue;
-            if (!per_point) {
-                other.push_back(c);
-                continue;
-            }
-            if (lazy_cd.empty()) {
-                lz.radius = c->lazy_radius;
-                lz.max_nn = c->lazy_max_nn;
-            }
-            if (c->lazy_radius != lz.radius || c->lazy_max_nn != lz.max_nn) {
-                other.push_back(c);
-                continue;
-            }
-            cdev[k].nstate = c->d_nstate;
-            cdev[k].lazy_blk0 = lz.tb;
-            tb_off.push_back(lz.tb);
-            lazy_cd.push_back(int32_t(k));
-            pt_off.push_back(lz.npts);
-            lz.tb += int32_t((c->n + 255) / 256);
-            lz.npts += c->n;
-        }
-        if (!other.empty() && (rc = lsm_normals_complete(ctx, other))) return rc;
-        tb_off.push_back(lz.tb);
-        lz.nl = int(lazy_cd.size());
+        std::vector<Cloud *> pending;
+        for (size_t k = 0; k < uniq.size(); ++k)
+            if (is_tgt[k] && uniq[k]->lazy) pending.push_back(uniq[k]);
+        if (!pending.empty() && (rc = lsm_normals_complete(ctx, pending))) return rc;
     }
 
     // pair states; block tasks are rebuilt for the active pairs of each pass (XCD-grouped: all
@@ -1592,32 +1536,6 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     PairState *d_ps;
     double *d_pbytes;
     if ((rc = upload(ctx, "i_cd", cdev, &d_cd))) return rc;
-    if (lz.nl > 0) {
-        int32_t *d_tboff, *d_lcd;
-        if ((rc = upload(ctx, "i_lz_off", tb_off, &d_tboff))) return rc;
-        if ((rc = upload(ctx, "i_lz_cd", lazy_cd, &d_lcd))) return rc;
-        int64_t *d_ptoff;
-        if ((rc = upload(ctx, "i_lz_pt", pt_off, &d_ptoff))) return rc;
-        lz.tb_off = d_tboff;
-        lz.lazy_cd = d_lcd;
-        lz.pt_off = d_ptoff;
-        const size_t ncnt_lz = size_t(max_iter + 2);
-        lz.blkflag = (uint8_t *)ctx->buf("i_lz_flag", size_t(lz.tb) + 1);
-        lz.list = (uint32_t *)ctx->buf("i_lz_list", size_t(lz.tb) * 4 + 4);
-        lz.counters = (uint32_t *)ctx->buf("i_lz_cnt", ncnt_lz * 8);
-        lz.cloud_cnt = (uint32_t *)ctx->buf("i_lz_ccnt", ncnt_lz * size_t(lz.nl) * 4);
-        lz.woff = (uint32_t *)ctx->buf("i_lz_woff", ncnt_lz * size_t(lz.nl + 1) * 4);
-        lz.plist = (int32_t *)ctx->buf("i_lz_plist", size_t(lz.npts) * 4 + 4);
-        if (!lz.blkflag || !lz.list || !lz.counters || !lz.cloud_cnt || !lz.woff || !lz.plist) {
-            ctx->set_error("scratch allocation failed (lazy normals)");
-            return LSM_ENOMEM;
-        }
-        LSM_HIP_TRY(ctx, hipMemsetAsync(lz.cloud_cnt, 0, ncnt_lz * size_t(lz.nl) * 4, st));
-        lz.host_count = (uint32_t *)ctx->host_pinned_extra(64);
-        if (!lz.host_count) return LSM_ENOMEM;
-        LSM_HIP_TRY(ctx, hipMemsetAsync(lz.blkflag, 0, size_t(lz.tb) + 1, st));
-        LSM_HIP_TRY(ctx, hipMemsetAsync(lz.counters, 0, size_t(max_iter + 2) * 8, st));
-    }
     if ((rc = upload(ctx, "i_ps", ps, &d_ps))) return rc;
     if ((rc = upload(ctx, "i_pbytes", pbytes, &d_pbytes))) return rc;
     const size_t nsrc_tot = size_t(std::max<int64_t>(src_off, 1));
@@ -1662,32 +1580,29 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     prm.max_iter = max_iter;
     prm.rel_fit = p.relative_fitness;
     prm.rel_rmse = p.relative_rmse;
-    {   // LSM_NN_SPLIT (read per call; the tests switch it): 1 = one lane per query
-        const char *e = getenv("LSM_NN_SPLIT");
-        const int v = e ? atoi(e) : 8;
+    // Search-path knobs (lsm_knob: test knobs, read per call; the tests switch them to prove
+    // every search path exact -- the shipped values are the defaults):
+    {   // LSM_NN_SPLIT: lanes per split box search (1 = one lane per query), LSM_NN_SPLIT_PLACE
+        const int v = int(lsm_knob("LSM_NN_SPLIT", 8));
         int l = 1;
         while (l * 2 <= v && l < 64) l *= 2;
         prm.split_max = l;
     }
-    prm.split_place = getenv("LSM_NN_SPLIT_PLACE") ? atoi(getenv("LSM_NN_SPLIT_PLACE")) : 0;
-    auto envf = [](const char *k, double d) {
-        const char *e = getenv(k);
-        return e ? atof(e) : d;
-    };
-    static const double M0 = envf("LSM_NN_M0", 0.0), MMUL = envf("LSM_NN_MMUL", 1.0),
-                        MADD = envf("LSM_NN_MADD", 1e-3);
-    prm.m0 = float(M0);
-    static const uint32_t LIN = uint32_t(envf("LSM_NN_LINEAR", 8));
-    prm.lin = LIN;
-    prm.m_mul = MMUL;
-    prm.m_add = MADD;
-    {   // LSM_NN_DIRECT (read per call): warm-start distance in cells from which a query goes
-        // straight to the fallback; <= 0 turns it off
-        const double d = envf("LSM_NN_DIRECT", NN_DIRECT_RC);
+    prm.split_place = int(lsm_knob("LSM_NN_SPLIT_PLACE", 0));
+    // certificate margin m = m_mul * delta + m_add (sweeps: DESIGN.md §7), pass-0 margin m0,
+    // entry searches linear below `lin` points
+    prm.m0 = 0.f;
+    prm.lin = 8;
+    prm.m_mul = 1.0;
+    prm.m_add = 1e-3;
+    {   // LSM_NN_DIRECT: warm-start distance in cells from which a query goes straight to the
+        // fallback (<= 0: off) once a pair has made LSM_NN_DIRECT_ITER updates; LSM_NN_KCOLD /
+        // LSM_NN_KMAX: the cold / warm box caps
+        const double d = lsm_knob("LSM_NN_DIRECT", NN_DIRECT_RC);
         prm.direct_rc = d > 0.0 ? float(d) : INFINITY;
-        prm.direct_iter = int(envf("LSM_NN_DIRECT_ITER", NN_DIRECT_ITER));
-        prm.kcold = std::max(1, int(envf("LSM_NN_KCOLD", NN_KCOLD)));
-        prm.kmax = std::max(1, int(envf("LSM_NN_KMAX", NN_KMAX)));
+        prm.direct_iter = int(lsm_knob("LSM_NN_DIRECT_ITER", NN_DIRECT_ITER));
+        prm.kcold = std::max(1, int(lsm_knob("LSM_NN_KCOLD", NN_KCOLD)));
+        prm.kmax = std::max(1, int(lsm_knob("LSM_NN_KMAX", NN_KMAX)));
     }
 
     // Passes are launched back to back; the plan of each pass is rebuilt on the device after the
@@ -1700,14 +1615,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int grid = int(std::max<int64_t>(per0 * NXCD, NXCD));
     int32_t *h_poll = (int32_t *)ctx->host_pinned(size_t(ncnt) * 3 * 4);
     if (!h_poll) return LSM_ENOMEM;
-    // LSM_POLL_COPY=1: read the poll words back with two copies per pass (the old path) instead
-    // of plan_kernel storing them into the mapped pinned buffer
-    static const bool poll_copy = getenv("LSM_POLL_COPY") && atoi(getenv("LSM_POLL_COPY")) != 0;
+    // plan_kernel stores the poll words into this mapped pinned buffer (no copy dispatches)
     int32_t *d_poll = nullptr;
-    if (!poll_copy) {
-        std::memset(h_poll, 0xff, size_t(ncnt) * 3 * 4);
-        LSM_HIP_TRY(ctx, hipHostGetDevicePointer((void **)&d_poll, h_poll, 0));
-    }
+    std::memset(h_poll, 0xff, size_t(ncnt) * 3 * 4);
+    LSM_HIP_TRY(ctx, hipHostGetDevicePointer((void **)&d_poll, h_poll, 0));
     std::vector<hipEvent_t> pass_ev(size_t(ncnt), nullptr);
     int passes = 0, polled = 0;
     // the recorded pass events go back to the context's pool on every return, early ones included
@@ -1720,25 +1631,23 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
     } ev_return{ctx, pass_ev, passes};
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
-    // search-path knobs are read per call (the tests switch them to prove every path exact)
-    const int FB_LANES = int(envf("LSM_NN_FB", 32));   // lanes per (near) fallback query
-    const double FB_FAR = envf("LSM_NN_FB_FAR", 0.0);   // m; 0: one kernel for all items
-    static const int PASS_LAG = [] {   // passes queued ahead of the last one read back
-        const char *e = getenv("LSM_PASS_LAG");
-        return e ? std::max(1, atoi(e)) : 2;
-    }();
+    constexpr int PASS_LAG = 2;   // passes queued ahead of the last one read back
     // LSM_NN_NOCERT=1: search every query in every pass (no stability certificate) -- the
     // tests' proof that certified passes return bit-identical correspondences
-    // passes before CERT_FROM search every query without the stability check: pass 1 follows
-    // the first update, which moves the scans by centimetres to decimetres -- beyond nearly
-    // every certificate -- so the check would only add its loads before the search
-    const int CERT_FROM = std::max(1, int(envf("LSM_NN_CERT_FROM", 2)));
-    const char *nc_env = getenv("LSM_NN_NOCERT");
-    const bool nocert = nc_env && atoi(nc_env) != 0;
+    // passes before LSM_NN_CERT_FROM search every query without the stability check: pass 1
+    // follows the first update, which moves the scans by centimetres to decimetres -- beyond
+    // nearly every certificate -- so the check would only add its loads before the search
+    const int CERT_FROM = std::max(1, int(lsm_knob("LSM_NN_CERT_FROM", 2)));
+    const bool nocert = lsm_knob("LSM_NN_NOCERT", 0) != 0.0;
     double ms0 = 0.0;
     for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
-    static const bool nn_stats = getenv("LSM_NN_STATS") != nullptr;
     unsigned long long *d_nst = nullptr;
+#ifdef LSM_DIAG
+    // diagnostics builds: per-pass search statistics to stderr (LSM_NN_STATS)
+    static const bool nn_stats = getenv("LSM_NN_STATS") != nullptr;
+#else
+    constexpr bool nn_stats = false;
+#endif
     if (nn_stats) {
         d_nst = (unsigned long long *)ctx->buf("i_nnstats", size_t(ncnt) * (NN_NSTAT + 8) * 8);
         if (!d_nst) return LSM_ENOMEM;
@@ -1767,57 +1676,32 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
         if (done) break;
         hipEvent_t ev;
-        // LSM_NN_XLDS=<bytes> (diagnostics, read per call): extra dynamic LDS per workgroup,
-        // lowering the correspondence kernel's occupancy (the occupancy-sensitivity probe)
-        const char *nxl = getenv("LSM_NN_XLDS");
-        const size_t nn_xlds = nxl ? size_t(atol(nxl)) : 0;
         ctx->tic("nn", &ev);
         if (d_nst) {
             unsigned long long *sp = d_nst + size_t(pass) * NN_NSTAT;
             if (pass < CERT_FROM || nocert)
                 nn_kernel<false, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass,
-                    lz.blkflag, sp);
+                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
             else
                 nn_kernel<true, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass,
-                    lz.blkflag, sp);
+                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
         } else if (pass < CERT_FROM || nocert)
-            nn_kernel<false><<<grid, NN_THREADS, nn_xlds, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt,
+            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt,
                                                                 d_cert, d_q, d_qn + pass, qcap,
-                                                                d_sqn + pass, lz.blkflag);
+                                                                d_sqn + pass);
         else
-            nn_kernel<true><<<grid, NN_THREADS, nn_xlds, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt,
+            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt,
                                                                d_cert, d_q, d_qn + pass, qcap,
-                                                               d_sqn + pass, lz.blkflag);
+                                                               d_sqn + pass);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
         {
             unsigned long long *fst = d_nst ? d_nst + size_t(ncnt) * NN_NSTAT + size_t(pass) * 8
                                             : nullptr;
-            // near items (box-search best within FB_FAR metres) with FB_LANES lanes each, the
-            // rest with a whole wave each (wide rings); every item is taken by exactly one
-            const float far2 = FB_FAR > 0.0 ? float(FB_FAR * FB_FAR) : INFINITY;
-            if (FB_LANES == 16)
-                nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst, far2, 0,
-                                                                lz.blkflag);
-            else if (FB_LANES == 32)
-                nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst, far2, 0,
-                                                                lz.blkflag);
-            else
-                nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst, far2, 0,
-                                                                lz.blkflag);
-            if (FB_LANES != 64 && FB_FAR > 0.0)
-                nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                                qcap, d_corr, d_cert, fst, far2, 1,
-                                                                lz.blkflag);
+            nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                            qcap, d_corr, d_cert, fst, INFINITY, 0);
         }
         ctx->toc("nn_fallback", ev);
-        // lazy normals: the target normals this pass's correspondences reach, before accumulate
-        if (lz.nl > 0 && (rc = lsm_normals_lazy_pass(ctx, lz, d_cd, pass))) return rc;
         ctx->tic("accumulate", &ev);
         if (p.method == LSM_P2PLANE)
             accumulate_kernel<LSM_P2PLANE><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, d_corr,
@@ -1831,16 +1715,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                                                        d_active + pass, d_bytes + pass,
                                                        d_srcn + pass, d_flags);
         ctx->toc("solve", ev);
-        if (d_poll) {
-            plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_coarse, d_plan,
-                                                    d_active + pass, d_poll + 3 * pass);
-        } else {
-            plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_coarse, d_plan);
-            LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass, d_active + pass, 4,
-                                            hipMemcpyDeviceToHost, st));
-            LSM_HIP_TRY(ctx, hipMemcpyAsync(h_poll + 3 * pass + 1, d_plan, 4,
-                                            hipMemcpyDeviceToHost, st));
-        }
+        plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_coarse, d_plan,
+                                                d_active + pass, d_poll + 3 * pass);
         pass_ev[size_t(pass)] = ctx->get_event();
         LSM_HIP_TRY(ctx, hipEventRecord(pass_ev[size_t(pass)], st));
         ++passes;
@@ -1928,6 +1804,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         ctx->stats["nn_queries_first_pass"].launches += queries0;
         ctx->stats["nn_pending"].launches += pend;
         ctx->stats["nn_pending_first_pass"].launches += passes > 0 ? qn[0] : 0;
+#ifdef LSM_DIAG
         if (getenv("LSM_DEBUG_PASSES")) {   // per pass: active pairs, searched, fallback
             std::vector<uint32_t> act(passes);
             LSM_HIP_TRY(ctx, hipMemcpy(act.data(), d_active, size_t(passes) * 4,
@@ -1936,6 +1813,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                 fprintf(stderr, "pass %2d: active-after %4u  searched %8u  fallback %7u\n", k,
                         act[k], sq[k], qn[k]);
         }
+#endif
     }
     for (int64_t k = 0; k < npairs; ++k) {
         const PairState &P = ps[k];

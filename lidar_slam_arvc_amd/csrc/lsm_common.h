@@ -32,12 +32,6 @@ struct CloudDev {
     int n;
     const uint32_t *perm;       // sorted position -> reference order
     const float4 *prior_ref;    // prior normals in reference order (orientation), or nullptr
-    // lazy normals (lsm_prep_params.want_normals = LSM_NORMALS_LAZY), set only in an ICP batch's
-    // copy of a P2Plane target: per point 0 = pending, 1 = needed this pass, 2 = computed; and
-    // the cloud's first 256-point block in the batch's block-flag table
-    uint8_t *nstate;
-    int32_t lazy_blk0;
-    int32_t pad_;
 };
 
 #define LSM_XYZ_PAD 16     // spare float4 points allocated past every processed cloud's end

@@ -35,8 +35,6 @@ struct Cloud {
     int64_t fpfh_cap = 0, fpfh_n = 0;
     float4 *d_prior_ref = nullptr; // prior normals (reference order) of a split cloud
     int64_t prior_n = 0;
-    uint8_t *d_nstate = nullptr;  // lazy normals: per point 0 pending, 1 needed, 2 computed
-    int64_t nstate_cap = 0;
     bool lazy = false;            // normals of some points still pending (computed on demand)
     double lazy_radius = 0.3;     // the KDTreeSearchParamHybrid of the pending normals
     int lazy_max_nn = 300;
@@ -66,6 +64,7 @@ struct lsm_ctx {
 
     // instrumentation
     bool timing = false;
+    bool statistics = false;      // lsm_set_timing(ctx, 2): also count the normals' neighbours
     std::map<std::string, KStat> stats;
     struct Pending {
         std::string name;
@@ -108,31 +107,10 @@ int lsm_loop_candidates_run(lsm_ctx *ctx, const double *positions, int64_t m, do
 int lsm_loop_partners_run(lsm_ctx *ctx, const double *positions, int64_t m,
                           const int64_t *cand, int64_t ncand, int64_t *partner);
 int lsm_download_run(lsm_ctx *ctx, Cloud *c, double *xyz, double *nrm, int64_t cap);
+// test knob `name` (api.cpp's list; environment, read per call) or dflt
+double lsm_knob(const char *name, double dflt);
 // lazy normals: compute every pending normal of the clouds (any use other than the ICP's)
 int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds);
-// lazy normals inside an ICP pass: the 256-point blocks flagged by this pass's correspondence
-// search (blkflag[tb]; cloud u's blocks start at tb_off[u], its CloudDev index is lazy_cd[u])
-// are listed, their needed points gathered per cloud (plist, cloud u's region from pt_off[u])
-// and computed by full waves. Per-pass slices: counters (2 u32), cloud_cnt (nl), woff (nl + 1),
-// all zeroed before the first pass.
-struct LazyNormals {
-    uint8_t *blkflag = nullptr;
-    uint32_t *list = nullptr;
-    uint32_t *counters = nullptr;
-    uint32_t *cloud_cnt = nullptr;
-    uint32_t *woff = nullptr;
-    int32_t *plist = nullptr;
-    const int32_t *tb_off = nullptr;   // [nl + 1]
-    const int32_t *lazy_cd = nullptr;  // [nl]
-    const int64_t *pt_off = nullptr;   // [nl]
-    int nl = 0;
-    int32_t tb = 0;
-    int64_t npts = 0;                  // points of the lazy targets (plist entries)
-    double radius = 0.3;
-    int max_nn = 300;
-    uint32_t *host_count = nullptr;    // pinned word: the pass's wave count
-};
-int lsm_normals_lazy_pass(lsm_ctx *ctx, const LazyNormals &lz, const CloudDev *cds, int pass);
 int lsm_ground_plane_run(lsm_ctx *ctx, Cloud *c, double height, double thr, int64_t iters,
                          uint64_t seed, double probability, double plane[4], int64_t *n_inliers,
                          int64_t *n_subset);

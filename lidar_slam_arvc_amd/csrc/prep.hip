@@ -594,10 +594,27 @@ __device__ __forceinline__ void cum_add_pt(Cum &c, float4 p, double qx, double q
     c.n += 1;
 }
 
-// prior (nullable): EstimateNormals on a cloud that already has normals -- a zero normal keeps
-// the prior one, and the new normal is flipped when it points against the prior.
+// Neighbourhoods of at most NSMALL points take Open3D's own covariance arithmetic
+// (normals_small_kernel): normal_from_cum marks them with w = 1 for that pass.
+constexpr int NSMALL = 16;
+
+// The normal of covariance A. prior (nullable): EstimateNormals on a cloud that already has
+// normals -- a zero normal keeps the prior one, and the new normal is flipped when it points
+// against the prior.
+__device__ __forceinline__ float4 normal_from_cov(const sym3 &A, const float4 *prior, float w) {
+    d3 v = fast_eigen3x3_min(A);
+    if (sqrt(d3_dot(v, v)) == 0.0) {
+        if (prior) return make_float4(prior->x, prior->y, prior->z, w);
+        v = {0.0, 0.0, 1.0};
+    }
+    if (prior && v.x * double(prior->x) + v.y * double(prior->y) + v.z * double(prior->z) < 0.0)
+        v = {-v.x, -v.y, -v.z};
+    return make_float4(float(v.x), float(v.y), float(v.z), w);
+}
+
 __device__ __forceinline__ float4 normal_from_cum(const Cum &c, const float4 *prior = nullptr) {
     sym3 A;
+    const float small = (c.n >= 3 && c.n <= NSMALL) ? 1.f : 0.f;
     if (c.n >= 3) {
         const double inv = 1.0 / double(c.n);
         const double mx = c.sx * inv, my = c.sy * inv, mz = c.sz * inv;
@@ -610,14 +627,7 @@ __device__ __forceinline__ float4 normal_from_cum(const Cum &c, const float4 *pr
     } else {
         A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
     }
-    d3 v = fast_eigen3x3_min(A);
-    if (sqrt(d3_dot(v, v)) == 0.0) {
-        if (prior) return make_float4(prior->x, prior->y, prior->z, 0.f);
-        v = {0.0, 0.0, 1.0};
-    }
-    if (prior && v.x * double(prior->x) + v.y * double(prior->y) + v.z * double(prior->z) < 0.0)
-        v = {-v.x, -v.y, -v.z};
-    return make_float4(float(v.x), float(v.y), float(v.z), 0.f);
+    return normal_from_cov(A, prior, small);
 }
 
 // Cell range of [q - h, q + h] along one axis, widened by a small margin so every point within
@@ -1005,135 +1015,29 @@ struct NPhase {
 //   NL_DENSE:  a deferred point, as NL_AUTO runs a predicted-dense one (scan 1 builds the
 //              histogram only; a point with count <= max_nn then takes the final pass whole,
 //              which adds its ball in scan 1's order -- NL_AUTO's sums for either prediction).
-//   NL_COOP:   NL_DENSE with scan 1 and the final pass run cooperatively by the wave
-//              (coop_visit); every lane of the wave must call it (`act` false: no point).
 // Returns false when the point was deferred.
 //   NL_DENSE_NR: NL_DENSE without the refine scans: a point that needs one (a saturated u8 bin, or
 //              a chosen bin holding more than SEL_CAP members: 0.002 % of the dense points) is
 //              deferred (returns false) to normals_refine_kernel, which runs it as NL_DENSE. The
 //              refine scans' live state sets the dense kernel's register count (101 VGPRs, 93
 //              without them): leaving them out lets the dense half run 5 waves per SIMD.
-constexpr int NL_AUTO = 0, NL_SPARSE = 1, NL_DENSE = 2, NL_COOP = 3, NL_DENSE_NR = 4;
+constexpr int NL_AUTO = 0, NL_SPARSE = 1, NL_DENSE = 2, NL_DENSE_NR = 4;
 #ifndef LSM_NDIAG
 #define LSM_NDIAG 0   // diagnostics builds only (wrong normals): 1 / 3 stop the dense half after
                       // scan 1 (3: without its histogram adds), 2 before its final pass
 #endif
 
-// wave-uniform min / max (readfirstlane: the result is known uniform, an SGPR value)
-__device__ __forceinline__ int wave_uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ float wave_minf(float v) {
-    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, LSM_WAVE));
-    return __int_as_float(wave_uni(__float_as_int(v)));
-}
-__device__ __forceinline__ float wave_maxf(float v) {
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, LSM_WAVE));
-    return __int_as_float(wave_uni(__float_as_int(v)));
-}
-__device__ __forceinline__ int wave_mini(int v) {
-    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, LSM_WAVE));
-    return wave_uni(v);
-}
-__device__ __forceinline__ int wave_maxi(int v) {
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, LSM_WAVE));
-    return wave_uni(v);
-}
-__device__ __forceinline__ float lane_f(float v, int i) {   // lane i's v (i wave-uniform)
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
-}
-
-// Cooperative visit of the balls of a wave's 64 points (radius rad per lane; lanes with !act
-// take no part): the rows of the union of their ball boxes in ball_visit_runs' order (z, then
-// y, then the row's block parts left to right), each row's runs loaded 64 points at a time
-// (one coalesced load per chunk) and cut to the union of the lanes' x windows by two ballots
-// (the runs are x-sorted). Every lane tests every candidate of the chunk, broadcast from its
-// lane in order: cls(p, k) classifies it for this lane (and returns true when the point is to be
-// added); the lane's adds of the chunk then run in order, add(p, k), in a loop of the wave's
-// maximum add count in which every lane takes part in the broadcast. A lane thus sees its ball
-// points in exactly the order of its own ball_visit_runs walk -- the same classifications, the
-// same cumulant sums -- from candidates it does not have to chase one memory round trip at a
-// time. Points outside a lane's ball are rejected by its own exact tests (the per-lane windows
-// were only a pruning device).
-template <typename Cls, typename Add>
-__device__ __forceinline__ void coop_visit(const CloudDev &C, float4 qf, float rad, bool act,
-                                           Cls &&cls, Add &&add) {
-    int ylo, yhi, zlo, zhi;
-    axis_range(qf.y, C.oy, C.inv_cell, rad, C.ny, ylo, yhi);
-    axis_range(qf.z, C.oz, C.inv_cell, rad, C.nz, zlo, zhi);
-    if (!act) {
-        ylo = zlo = 0x7fffffff;
-        yhi = zhi = -1;
-    }
-    const int Zlo = wave_mini(zlo), Zhi = wave_maxi(zhi);
-    const int Ylo = wave_mini(ylo), Yhi = wave_maxi(yhi);
-    const float prune = rad * 1.0001f + 1e-6f;
-    const float prune2 = prune * prune;
-    const int lane = __lane_id();
-#pragma unroll 1
-    for (int z = Zlo; z <= Zhi; ++z) {
-        const float dz2 = slab_d2(qf.z, C.oz, C.cell, z);
-#pragma unroll 1
-        for (int y = Ylo; y <= Yhi; ++y) {
-            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
-            const bool need = act && z >= zlo && z <= zhi && y >= ylo && y <= yhi && !(dyz2 > prune2);
-            if (__ballot(need) == 0) continue;
-            float xl = INFINITY, xh = -INFINITY;
-            if (need) {   // the row's chord window, as ball_visit_runs widens it
-                const float ch = sqrtf(prune2 - dyz2) * 1.0001f + 1e-6f * fabsf(qf.x) + 1e-5f;
-                xl = qf.x - ch;
-                xh = qf.x + ch;
-            }
-            const float XL = wave_minf(xl), XH = wave_maxf(xh);
-            // the cells of x in [XL, XH] (slack for the f32 cell coordinates, as axis_range)
-            const int xa = max((int)floorf((XL - C.ox) * C.inv_cell - 1e-3f), 0);
-            const int xb = min((int)floorf((XH - C.ox) * C.inv_cell + 1e-3f), C.nx - 1);
-            int x = xa;
-#pragma unroll 1
-            while (x <= xb) {
-                const int xe = wave_uni(min(xb, x | (LSM_BLK - 1)));
-                const uint32_t a = lsm_ld(C.cell_start, lsm_cell_lin(C.nbx, C.nby, x, y, z));
-                const uint32_t b = lsm_ld(C.cell_start, lsm_cell_lin(C.nbx, C.nby, xe, y, z) + 1);
-                x = xe + 1;
-#pragma unroll 1
-                for (uint32_t pos = a; pos < b; pos += LSM_WAVE) {
-                    const uint32_t cnt = min(uint32_t(LSM_WAVE), b - pos);
-                    const float4 c = lsm_ld(C.xyz, pos + min(uint32_t(lane), cnt - 1));
-                    const bool valid = uint32_t(lane) < cnt;
-                    const int i0 = __popcll(__ballot(valid && c.x < XL));
-                    const int i1 = __popcll(__ballot(valid && !(c.x > XH)));
-                    uint64_t addm = 0;
-#pragma unroll 2
-                    for (int i = i0; i < i1; ++i) {
-                        const float4 p = make_float4(lane_f(c.x, i), lane_f(c.y, i), lane_f(c.z, i), 0.f);
-                        if (act && cls(p, pos + uint32_t(i))) addm |= uint64_t(1) << i;
-                    }
-                    const int rounds = wave_maxi(__popcll(addm));
-#pragma unroll 1
-                    for (int r = 0; r < rounds; ++r) {
-                        const bool has = addm != 0;
-                        const int i = has ? __ffsll((unsigned long long)addm) - 1 : 0;
-                        addm &= addm - 1;
-                        const float px = __shfl(c.x, i, LSM_WAVE), py = __shfl(c.y, i, LSM_WAVE),
-                                    pz = __shfl(c.z, i, LSM_WAVE);
-                        if (has) add(make_float4(px, py, pz, 0.f), pos + uint32_t(i));
-                    }
-                    if (i1 < int(cnt)) break;   // the rest of the run lies past every window
-                }
-            }
-        }
-    }
-}
-
 template <int G, typename Acc, bool PH = false, int MODE = NL_AUTO, int PF = LSM_NORMALS_PF>
 __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                             unsigned long long *stats, uint32_t *H, Acc &acc,
-                            NPhase *ph = nullptr, bool act = true) {
+                            NPhase *ph = nullptr) {
     const HRow R{H, HSTRIDE == 32 ? (__lane_id() & 31u) : 0u};
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
     const NormalsPts pts = normals_pts(C);
     // Dense-predicted points skip acc.add in scan 1 (histogram only); a wrong guess costs one
     // plain rescan below, which visits the ball in scan 1's order (identical sums).
-    const bool dense = (MODE == NL_DENSE || MODE == NL_COOP || MODE == NL_DENSE_NR) ? true : predict_dense(C, np, qf);
+    const bool dense = (MODE == NL_DENSE || MODE == NL_DENSE_NR) ? true : predict_dense(C, np, qf);
     if (MODE == NL_SPARSE && dense) return false;
     NP_ST(ph, 7, dense ? 1u : 0u);
     if (MODE != NL_SPARSE) {
@@ -1179,16 +1083,9 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
 #endif
             }
     };
-    if (MODE == NL_COOP) {
-        coop_visit(C, qf, np.r, act, [&](const float4 &p, uint32_t k) {
-            scan1(p, k, true);
-            return false;
-        }, [](const float4 &, uint32_t) {});
-    } else {
-        ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-            scan_run_pred<G, PF>(pts, a, b, xl, xh, scan1);
-        });
-    }
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+        scan_run_pred<G, PF>(pts, a, b, xl, xh, scan1);
+    });
     if (MODE == NL_SPARSE) {
         if (count > np.max_nn) return false;
         acc.finish();
@@ -1351,17 +1248,11 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
         }
         return false;
     };
-    if (MODE == NL_COOP) {
-        coop_visit(C, qf, sel_radius(top, np.r), act,
-                   [&](const float4 &p, uint32_t k) { return fin(p, k, true); },
-                   [&](const float4 &p, uint32_t k) { acc.add(p, k); });
-    } else {
-        ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
-            scan_run_pred<G, PF>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
-                if (fin(p, k, in)) acc.add(p, k);
-            });
+    ball_visit_runs(C, qf, sel_radius(top, np.r), [&](uint32_t a, uint32_t b, float xl, float xh) {
+        scan_run_pred<G, PF>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+            if (fin(p, k, in)) acc.add(p, k);
         });
-    }
+    });
     const uint32_t mm = m < SEL_CAP ? m : SEL_CAP;
     for (uint32_t e = 0; e < mm; ++e) {
         const uint32_t fe = R[2 * e];   // non-negative floats order like their bit patterns
@@ -1391,22 +1282,16 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
 // its ball (a performance guess only: both outcomes are exact): frac * max_nn * (cell / r)^2,
 // a surface's share of the ball in one cell. On HDL-64 scans with cell = r = 0.3 m and
 // max_nn = 300, frac = 0.27 mispredicts ~4 % of the ball work either way.
-// LSM_NORMALS_DENSE=<frac> overrides 0.27; 0 turns the prediction off.
+// (a bench sweep of frac over 0.20-0.45: 0.27 best)
+constexpr double NORMALS_DENSE_FRAC = 0.27;
 float dense_k(int max_nn, double r2) {
-    static const double frac = [] {
-        const char *e = getenv("LSM_NORMALS_DENSE");
-        return e ? atof(e) : 0.27;
-    }();
-    if (frac <= 0.0 || r2 <= 0.0) return 0.f;
-    return float(frac * double(max_nn) / r2);
+    if (r2 <= 0.0) return 0.f;
+    return float(NORMALS_DENSE_FRAC * double(max_nn) / r2);
 }
 
-// LSM_NORMALS_EXACT=1 (read per call): no f32 pre-classification in the final pass -- the tests'
-// proof that it leaves every neighbourhood, and so every normal, bit-identical
-int normals_preclass() {
-    const char *e = getenv("LSM_NORMALS_EXACT");
-    return (e && atoi(e) != 0) ? 0 : 1;
-}
+// LSM_NORMALS_EXACT=1 (a test knob, read per call): no f32 pre-classification in the final pass
+// -- the tests' proof that it leaves every neighbourhood, and so every normal, bit-identical
+int normals_preclass() { return lsm_knob("LSM_NORMALS_EXACT", 0.0) != 0.0 ? 0 : 1; }
 
 NormalParams normal_params(double radius, int max_nn) {
     NormalParams np;
@@ -1450,10 +1335,6 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
 // the list does not matter: every point's computation is independent of the others).
 // registers of the sparse half capped for 8 waves per SIMD (64 VGPRs; 14 spilled outside the
 // walks): normals 148.2 -> 143.8 ms per step (7 waves: 144.1; uncapped, 80 VGPRs: 6 waves)
-#ifndef LSM_NORMALS_WG_APPEND
-#define LSM_NORMALS_WG_APPEND 1
-#endif
-
 // Append point j (when `take`) to a cloud's list, one atomic per workgroup: the workgroup's
 // entries stay one run in lane order. Every thread of the workgroup must call it.
 __device__ __forceinline__ void wg_append(bool take, uint32_t j, uint32_t *list, uint32_t *cnt) {
@@ -1476,21 +1357,6 @@ __device__ __forceinline__ void wg_append(bool take, uint32_t j, uint32_t *list,
     __syncthreads();   // s_cnt is reused by the next call
 }
 
-// Split launch, stage 0 (LSM_NORMALS_CLASSIFY): the clouds' points into a sparse list and a
-// dense list by the density prediction, so the sparse half also runs in full waves.
-__global__ void __launch_bounds__(PT_THREADS)
-normals_classify_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
-                        uint32_t *slist, uint32_t *scnt, uint32_t *dlist, uint32_t *dcnt) {
-    const Seg s = segs[blockIdx.x];
-    const CloudDev C = cd[s.cloud];
-    const int j = s.start + threadIdx.x;
-    bool dense = false;
-    const bool valid = j < C.n;
-    if (valid) dense = predict_dense(C, np, lsm_ld(C.xyz, j));
-    const uint32_t off = geo[s.cloud].pt_off;
-    wg_append(valid && !dense, uint32_t(j), slist + off, scnt + s.cloud);
-    wg_append(valid && dense, uint32_t(j), dlist + off, dcnt + s.cloud);
-}
 #ifndef LSM_NSPARSE_WPE
 #define LSM_NSPARSE_WPE 8
 #endif
@@ -1499,23 +1365,14 @@ normals_classify_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo,
 #else
 #define LSM_NSPARSE_ATTR
 #endif
-template <int G, bool LIST = false>
+template <int G>
 __global__ void __launch_bounds__(PT_THREADS) LSM_NSPARSE_ATTR
 normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
-                      uint32_t *dlist, uint32_t *dcnt, unsigned long long *stats,
-                      const uint32_t *slist = nullptr, const uint32_t *scnt = nullptr) {
+                      uint32_t *dlist, uint32_t *dcnt, unsigned long long *stats) {
     const Seg s = segs[blockIdx.x];
     const CloudDev C = cd[s.cloud];
-    int j = s.start + threadIdx.x;
-    bool valid = j < C.n;
-    // lazy completion: a point whose normal an earlier per-point batch computed is skipped
-    if (!LIST && valid && C.nstate && C.nstate[j]) valid = false;
-    if (LIST) {   // LSM_NORMALS_CLASSIFY: entries of the cloud's sparse list
-        const uint32_t n = scnt[s.cloud];
-        if (uint32_t(s.start) >= n) return;   // the whole workgroup is past the list
-        valid = uint32_t(j) < n;
-        if (valid) j = int(slist[geo[s.cloud].pt_off + uint32_t(j)]);
-    }
+    const int j = s.start + threadIdx.x;
+    const bool valid = j < C.n;
     bool defer = false;
     if (valid) {
         const float4 q = lsm_ld(C.xyz, j);
@@ -1524,32 +1381,14 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
         defer = !hybrid_lane<G, CumAcc, false, NL_SPARSE>(C, j, np, nullptr, nullptr, acc);
         if (stats && !defer) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
     }
-    const uint64_t bm = __ballot(defer);
-    const int lane = threadIdx.x & 63;
-#if LSM_NORMALS_WG_APPEND
     // one append per workgroup: its deferred points stay one run in cell order (the dense
     // half's waves then hold neighbouring points)
-    (void)bm;
-    (void)lane;
     wg_append(defer, uint32_t(j), dlist + geo[s.cloud].pt_off, dcnt + s.cloud);
-#else
-    if (bm) {
-        const int leader = __ffsll((unsigned long long)bm) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(dcnt + s.cloud, uint32_t(__popcll(bm)));
-        base = __shfl(base, leader, LSM_WAVE);
-        if (defer)
-            dlist[geo[s.cloud].pt_off + base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = uint32_t(j);
-    }
-#endif
 }
 
 // Split launch, second half: one lane per entry of the clouds' dense lists (NL_DENSE), so the
 // truncated neighbourhoods run in full waves. The grid is the first half's (a cloud's list never
 // holds more entries than the cloud has points); workgroups past the list return at once.
-#ifndef LSM_NORMALS_DEFER_REFINE
-#define LSM_NORMALS_DEFER_REFINE 1
-#endif
 // LSM_NDENSE_WPE: waves per SIMD requested for the dense half (0: no request)
 #ifndef LSM_NDENSE_WPE
 #define LSM_NDENSE_WPE 0
@@ -1574,7 +1413,6 @@ normals_dense_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, No
     const float4 q = lsm_ld(C.xyz, j);
     CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
-#if LSM_NORMALS_DEFER_REFINE
     // the rare points that need a refine scan go to the cloud's refine list
     const bool done = hybrid_lane<G, CumAcc, false, NL_DENSE_NR, LSM_NORMALS_PFD>(
         C, j, np, stats, lds + threadIdx.x * HSTRIDE, acc);
@@ -1587,13 +1425,6 @@ normals_dense_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, No
         if (!done) rlist[off + base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = uint32_t(j);
     }
     if (stats && done) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
-#else
-    (void)rlist;
-    (void)rcnt;
-    hybrid_lane<G, CumAcc, false, NL_DENSE, LSM_NORMALS_PFD>(C, j, np, stats,
-                                                             lds + threadIdx.x * HSTRIDE, acc);
-    if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
-#endif
 }
 
 // The dense half's deferred points (NL_DENSE with its refine scans): blockIdx.x = cloud, the
@@ -1626,41 +1457,133 @@ template <int G>
 void launch_dense_half(hipStream_t st, const Seg *d_segs, int nseg, const CloudDev *d_cd,
                        const GridGeo *d_geo, int K, const NormalParams &np, const uint32_t *dlist,
                        const uint32_t *dcnt, unsigned long long *d_ns, uint32_t *rlist,
-                       uint32_t *rcnt, size_t xlds) {
-    normals_dense_kernel<G><<<nseg, PT_THREADS, xlds, st>>>(d_segs, d_cd, d_geo, np, dlist, dcnt,
-                                                            d_ns, rlist, rcnt);
-#if LSM_NORMALS_DEFER_REFINE
+                       uint32_t *rcnt) {
+    normals_dense_kernel<G><<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, d_geo, np, dlist, dcnt,
+                                                         d_ns, rlist, rcnt);
     normals_refine_kernel<G><<<dim3(K, REFINE_BLOCKS), PT_THREADS, 0, st>>>(d_cd, d_geo, np, rlist,
                                                                            rcnt, d_ns);
-#endif
 }
 
-// normals_dense_kernel with the scans run cooperatively by each wave (NL_COOP, coop_visit):
-// lanes past the list end ride along without a point (they shadow the wave's first entry and
-// write nothing). LSM_NORMALS_COOP=0 selects the per-lane walks.
-template <int G>
-__global__ void __launch_bounds__(PT_THREADS) LSM_NORMALS_ATTR
-normals_dense_coop_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
-                          const uint32_t *dlist, const uint32_t *dcnt, unsigned long long *stats) {
-    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
+// Small neighbourhoods in Open3D's arithmetic (keyframe.py:160-162 -> [O3D]
+// EstimatePerPointCovariances -> ComputeCovariance). A neighbourhood of a few points -- near-
+// collinear points of one distant ring -- has a rank-deficient covariance whose smallest
+// eigenvector the rounding of the cumulants decides, so the centred cumulants of the main path
+// (better numerics, different rounding) would pick a different normal there. For the points
+// normal_from_cum marked (3 <= n <= NSMALL; w = 1) a second pass redoes the neighbourhood exactly
+// as Open3D does: the ball's members in the search's order (ascending d2, ties by reference
+// index), the nine raw f64 cumulants summed in that order with every product rounded on its
+// own, each divided by n, cov = E[pp^T] - mu mu^T, FastEigen3x3 -- and clears the mark.
+//   stage 1 (normals_small_list_kernel): the marked points of a batch -> one list of (cloud,
+//           point), wave-aggregated appends (a wave's entries stay one run in cell order);
+//   stage 2 (normals_small_kernel): a fixed grid of one-wave workgroups strides over the list,
+//           the member lists in LDS (one slot column per lane).
+__global__ void __launch_bounds__(PT_THREADS)
+normals_small_list_kernel(const Seg *segs, const CloudDev *cd, uint2 *list, uint32_t *cnt) {
     const Seg s = segs[blockIdx.x];
-    const uint32_t n = dcnt[s.cloud];
-    const uint32_t slot = uint32_t(s.start) + threadIdx.x;
-    const uint32_t first = uint32_t(s.start) + (threadIdx.x & ~uint32_t(LSM_WAVE - 1));
-    if (first >= n) return;   // the whole wave is past the list
-    const bool act = slot < n;
-    const CloudDev C = cd[s.cloud];
-    const int j = int(dlist[geo[s.cloud].pt_off + (act ? slot : first)]);
-    const float4 q = lsm_ld(C.xyz, j);
-    CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z),
-               act ? const_cast<float4 *>(C.nrm) + j : nullptr,
-               C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
-    hybrid_lane<G, CumAcc, false, NL_COOP>(C, j, np, act ? stats : nullptr,
-                                           lds + threadIdx.x * HSTRIDE, acc, nullptr, act);
-    if (stats && act) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+    const int j = s.start + threadIdx.x;
+    const CloudDev &C = cd[s.cloud];
+    const bool take = j < C.n && lsm_ld(C.nrm, j).w != 0.f;
+    const uint64_t bm = __ballot(take);
+    if (!bm) return;
+    const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)bm) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(cnt, uint32_t(__popcll(bm)));
+    base = uint32_t(__shfl(int(base), leader, LSM_WAVE));
+    if (take) list[base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = make_uint2(uint32_t(s.cloud), uint32_t(j));
 }
 
-// normals_kernel with phase statistics (LSM_NORMALS_PHASES=1, diagnostics): per counter the
+constexpr int SMALL_WG = LSM_WAVE;
+__global__ void __launch_bounds__(SMALL_WG)
+normals_small_kernel(const CloudDev *cd, NormalParams np, const uint2 *list, const uint32_t *cnt) {
+    __shared__ double s_d2[NSMALL * SMALL_WG];
+    __shared__ uint32_t s_ref[NSMALL * SMALL_WG];
+    __shared__ uint32_t s_k[NSMALL * SMALL_WG];
+    double *D = s_d2 + threadIdx.x;
+    uint32_t *Rf = s_ref + threadIdx.x, *Kk = s_k + threadIdx.x;
+    const int cap = np.max_nn < NSMALL ? np.max_nn : NSMALL;
+    const uint32_t total = *cnt;
+    for (uint32_t e = blockIdx.x * SMALL_WG + threadIdx.x; e < total; e += gridDim.x * SMALL_WG) {
+        const uint2 it = list[e];
+        const CloudDev C = cd[it.x];   // per lane: a wave may span two clouds
+        const int j = int(it.y);
+        const float4 qf = lsm_ld(C.xyz, j);
+        const double qx = qf.x, qy = qf.y, qz = qf.z;
+        int m = 0;
+        const GlobalPts pts{C.xyz};
+        ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+            scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+                Off o;
+                if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
+                const uint32_t ref = lsm_ld(C.perm, k);
+                auto before = [&](int q) {   // (d2, ref) precedes entry q
+                    const double dq = D[q * SMALL_WG];
+                    return o.d2 < dq || (o.d2 == dq && ref < Rf[q * SMALL_WG]);
+                };
+                int pos;
+                if (m < cap) pos = m++;
+                else if (cap > 0 && before(cap - 1)) pos = cap - 1;
+                else return;
+                for (; pos > 0 && before(pos - 1); --pos) {
+                    D[pos * SMALL_WG] = D[(pos - 1) * SMALL_WG];
+                    Rf[pos * SMALL_WG] = Rf[(pos - 1) * SMALL_WG];
+                    Kk[pos * SMALL_WG] = Kk[(pos - 1) * SMALL_WG];
+                }
+                D[pos * SMALL_WG] = o.d2;
+                Rf[pos * SMALL_WG] = ref;
+                Kk[pos * SMALL_WG] = k;
+            });
+        });
+        double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0,
+               c8 = 0.0;
+        for (int q = 0; q < m; ++q) {
+            const float4 p = lsm_ld(C.xyz, Kk[q * SMALL_WG]);
+            const double x = p.x, y = p.y, z = p.z;
+            c0 = lsm_dadd(c0, x);
+            c1 = lsm_dadd(c1, y);
+            c2 = lsm_dadd(c2, z);
+            c3 = lsm_dadd(c3, lsm_dmul(x, x));
+            c4 = lsm_dadd(c4, lsm_dmul(x, y));
+            c5 = lsm_dadd(c5, lsm_dmul(x, z));
+            c6 = lsm_dadd(c6, lsm_dmul(y, y));
+            c7 = lsm_dadd(c7, lsm_dmul(y, z));
+            c8 = lsm_dadd(c8, lsm_dmul(z, z));
+        }
+        sym3 A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+        if (m >= 3) {
+            const double dn = double(m);
+            c0 = lsm_ddiv(c0, dn);
+            c1 = lsm_ddiv(c1, dn);
+            c2 = lsm_ddiv(c2, dn);
+            c3 = lsm_ddiv(c3, dn);
+            c4 = lsm_ddiv(c4, dn);
+            c5 = lsm_ddiv(c5, dn);
+            c6 = lsm_ddiv(c6, dn);
+            c7 = lsm_ddiv(c7, dn);
+            c8 = lsm_ddiv(c8, dn);
+            A.a00 = lsm_dsub(c3, lsm_dmul(c0, c0));
+            A.a01 = lsm_dsub(c4, lsm_dmul(c0, c1));
+            A.a02 = lsm_dsub(c5, lsm_dmul(c0, c2));
+            A.a11 = lsm_dsub(c6, lsm_dmul(c1, c1));
+            A.a12 = lsm_dsub(c7, lsm_dmul(c1, c2));
+            A.a22 = lsm_dsub(c8, lsm_dmul(c2, c2));
+        }
+        const_cast<float4 *>(C.nrm)[j] =
+            normal_from_cov(A, C.prior_ref ? C.prior_ref + C.perm[j] : nullptr, 0.f);
+    }
+}
+
+// The small-neighbourhood pass over the clouds of `segs` (one lane per point in stage 1).
+// list: scratch of one uint2 per point of the batch; cnt: one scratch word.
+void launch_small_normals(hipStream_t st, const Seg *d_segs, int nseg, const CloudDev *d_cd,
+                          const NormalParams &np, uint2 *list, uint32_t *cnt, int num_cus) {
+    if (nseg <= 0) return;
+    (void)hipMemsetAsync(cnt, 0, 4, st);
+    normals_small_list_kernel<<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, list, cnt);
+    normals_small_kernel<<<std::max(1, num_cus * 8), SMALL_WG, 0, st>>>(d_cd, np, list, cnt);
+}
+
+#ifdef LSM_DIAG
+// normals_kernel with phase statistics (LSM_NORMALS_PHASES=1, diagnostics builds): per counter the
 // lane sum (out[c]) and the per-wave maximum summed over waves (out[8 + c]: the wave's cost
 // under divergence)
 __global__ void __launch_bounds__(PT_THREADS)
@@ -1690,6 +1613,7 @@ normals_phase_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
         }
     }
 }
+#endif
 
 // Neighbour lists of FPFH (ComputeFPFHFeature's KDTreeSearchParamHybrid): at most `cap` per
 // point, row j of idx / d2 (sorted order), count[j].
@@ -1705,208 +1629,6 @@ nbr_lists_kernel(const Seg *segs, const CloudDev *cd, NormalParams np, int32_t *
     ListAcc acc{idx + size_t(j) * cap, d2 + size_t(j) * cap, count + j, cap, 0,
                 double(q.x), double(q.y), double(q.z)};
     hybrid_lane<NORMALS_G_DEFAULT>(C, j, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
-}
-
-// ------------------------------------------------------------------------------------------
-// lazy normals (LSM_NORMALS_LAZY): the normals a P2Plane ICP pass reaches, on demand
-// ------------------------------------------------------------------------------------------
-// One 256-point block of cloud C: the points whose normal is wanted (state 1 = needed this
-// pass, or every state but 2 = computed when completing) are compacted in LDS, in cell order,
-// and lanes [0, count) each compute one with the eager kernel's hybrid_lane -- so the waves stay
-// full and spatially coherent, and every normal is bit-identical to the eager one.
-template <int G>
-__device__ __forceinline__ void lazy_block(const CloudDev &C, uint8_t *nstate, int j0,
-                                           bool complete, const NormalParams &np, uint32_t *lds,
-                                           int32_t *s_idx, int32_t *s_cnt,
-                                           unsigned long long *stats = nullptr) {
-    const int j = j0 + int(threadIdx.x);
-    bool need = false;
-    if (j < C.n) {
-        const uint8_t st = nstate[j];
-        need = complete ? st != 2 : st == 1;
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t bm = __ballot(need);
-    if (lane == 0) s_cnt[w] = __popcll(bm);
-    __syncthreads();
-    int before = 0, total = 0;
-#pragma unroll
-    for (int q = 0; q < PT_THREADS / LSM_WAVE; ++q) {
-        before += q < w ? s_cnt[q] : 0;
-        total += s_cnt[q];
-    }
-    if (need) s_idx[before + __popcll(bm & ((uint64_t(1) << lane) - 1))] = j;
-    __syncthreads();
-    if (int(threadIdx.x) < total) {
-        const int jj = s_idx[threadIdx.x];
-        const float4 q = lsm_ld(C.xyz, jj);
-        CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + jj,
-                   C.prior_ref ? C.prior_ref + C.perm[jj] : nullptr};
-        hybrid_lane<G>(C, jj, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
-        nstate[jj] = 2;
-        if (stats) {   // statistics runs only: neighbours and normals computed
-            atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
-            atomicAdd(stats + 1, 1ull);
-        }
-    }
-    __syncthreads();   // s_idx / s_cnt are reused by the next block
-}
-
-// the blocks flagged by this pass's correspondence search (one flag byte per 256-point block of
-// the batch's lazy targets) -> list; flags cleared for the next pass
-__global__ void __launch_bounds__(256)
-lazy_compact_kernel(uint8_t *__restrict__ blkflag, int32_t tb, uint32_t *__restrict__ list,
-                    uint32_t *__restrict__ counters) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    bool f = false;
-    if (i < tb) {
-        f = blkflag[i] != 0;
-        if (f) blkflag[i] = 0;
-    }
-    const uint64_t bm = __ballot(f);
-    if (!bm) return;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((unsigned long long)bm) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(counters, uint32_t(__popcll(bm)));
-    base = __shfl(base, leader, LSM_WAVE);
-    if (f) list[base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = uint32_t(i);
-}
-
-// The listed blocks' needed points, gathered per cloud into full waves: one wave per listed
-// block (grid-stride) appends the block's needed points, in cell order, to its cloud's region
-// of the point list (pt_off[u] .. pt_off[u] + n_u) at an offset from one atomic per block.
-// (A block-per-workgroup form left the later passes' few needed points per block to waves of
-// one or two busy lanes: 3.5x the eager cost for 76 % of the normals.)
-__global__ void __launch_bounds__(256)
-lazy_gather_kernel(const CloudDev *__restrict__ cds, const int32_t *__restrict__ tb_off,
-                   const int32_t *__restrict__ lazy_cd, const int64_t *__restrict__ pt_off, int nl,
-                   const uint32_t *__restrict__ list, const uint32_t *__restrict__ counters,
-                   uint32_t *__restrict__ cloud_cnt, int32_t *__restrict__ plist) {
-    const uint32_t nb = counters[0];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t b = wave; b < nb; b += nwaves) {
-        const int32_t e = int32_t(list[b]);
-        int lo = 0, hi = nl;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (tb_off[mid] <= e) lo = mid;
-            else hi = mid;
-        }
-        const CloudDev C = cds[lazy_cd[lo]];
-        const int j0 = (e - tb_off[lo]) * PT_THREADS;
-        bool need[PT_THREADS / LSM_WAVE];
-        uint64_t bm[PT_THREADS / LSM_WAVE];
-        uint32_t tot = 0;
-#pragma unroll
-        for (int q = 0; q < PT_THREADS / LSM_WAVE; ++q) {
-            const int j = j0 + q * LSM_WAVE + lane;
-            need[q] = j < C.n && C.nstate[j] == 1;
-            bm[q] = __ballot(need[q]);
-            tot += uint32_t(__popcll(bm[q]));
-        }
-        if (tot == 0) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(cloud_cnt + lo, tot);
-        base = __shfl(base, 0, LSM_WAVE);
-        int32_t *out = plist + pt_off[lo] + base;
-#pragma unroll
-        for (int q = 0; q < PT_THREADS / LSM_WAVE; ++q) {
-            if (need[q]) out[__popcll(bm[q] & ((uint64_t(1) << lane) - 1))] = j0 + q * LSM_WAVE + lane;
-            out += __popcll(bm[q]);
-        }
-    }
-}
-
-// per lazy cloud: waves of 64 gathered points; exclusive prefix over the clouds (one
-// workgroup), the total for the host (counters[1])
-__global__ void __launch_bounds__(1024)
-lazy_waves_kernel(const uint32_t *__restrict__ cloud_cnt, int nl, uint32_t *__restrict__ woff,
-                  uint32_t *__restrict__ counters) {
-    __shared__ uint32_t wsum[1024 / LSM_WAVE];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t carry = 0;
-    for (int base = 0; base < nl; base += 1024) {
-        const int k = base + threadIdx.x;
-        const uint32_t v = k < nl ? (cloud_cnt[k] + LSM_WAVE - 1) / LSM_WAVE : 0;
-        uint32_t x = v;
-#pragma unroll
-        for (int off = 1; off < LSM_WAVE; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off, LSM_WAVE);
-            if (lane >= off) x += y;
-        }
-        if (lane == LSM_WAVE - 1) wsum[w] = x;
-        __syncthreads();
-        uint32_t before = carry, tot = 0;
-        for (int q = 0; q < 1024 / LSM_WAVE; ++q) {
-            before += q < w ? wsum[q] : 0;
-            tot += wsum[q];
-        }
-        if (k < nl) woff[k] = before + x - v;
-        carry += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        woff[nl] = carry;
-        counters[1] = carry;
-    }
-}
-
-// one wave per 64 gathered points of one cloud (the cloud is wave-uniform: SGPR descriptor,
-// as the eager kernel's workgroup-uniform one); each lane computes one normal exactly as the
-// eager normals_kernel does
-__global__ void __launch_bounds__(PT_THREADS)
-lazy_normals_kernel(const CloudDev *__restrict__ cds, const int32_t *__restrict__ lazy_cd,
-                    const int64_t *__restrict__ pt_off, int nl, NormalParams np,
-                    const uint32_t *__restrict__ woff, const uint32_t *__restrict__ cloud_cnt,
-                    const int32_t *__restrict__ plist, unsigned long long *stats) {
-    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
-    const int lane = threadIdx.x & 63;
-    const uint32_t gw = uint32_t(__builtin_amdgcn_readfirstlane(
-        int(blockIdx.x * (PT_THREADS / LSM_WAVE) + (threadIdx.x >> 6))));
-    if (gw >= woff[nl]) return;
-    int lo = 0, hi = nl;   // the cloud u with woff[u] <= gw < woff[u + 1]
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (woff[mid] <= gw) lo = mid;
-        else hi = mid;
-    }
-    lo = __builtin_amdgcn_readfirstlane(lo);
-    const uint32_t entry = (gw - woff[lo]) * LSM_WAVE + uint32_t(lane);
-    if (entry >= cloud_cnt[lo]) return;
-    const CloudDev C = cds[lazy_cd[lo]];
-    const int j = plist[pt_off[lo] + entry];
-    const float4 q = lsm_ld(C.xyz, j);
-    CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
-               C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
-    hybrid_lane<NORMALS_G_DEFAULT>(C, j, np, nullptr, lds + threadIdx.x * HSTRIDE, acc);
-    C.nstate[j] = 2;
-    if (stats) {   // statistics runs only: neighbours and normals computed
-        atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
-        atomicAdd(stats + 1, 1ull);
-    }
-}
-
-// completion: every pending normal of the listed clouds (one workgroup per 256-point segment)
-__global__ void __launch_bounds__(PT_THREADS)
-complete_normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
-                        unsigned long long *stats) {
-    __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
-    __shared__ int32_t s_idx[PT_THREADS];
-    __shared__ int32_t s_cnt[PT_THREADS / LSM_WAVE];
-    const Seg s = segs[blockIdx.x];
-    const CloudDev C = cd[s.cloud];
-    lazy_block<NORMALS_G_DEFAULT>(C, C.nstate, s.start, true, np, lds, s_idx, s_cnt, stats);
-}
-
-__global__ void __launch_bounds__(PT_THREADS)
-nstate_zero_kernel(const Seg *segs, const CloudDev *cd) {
-    const Seg s = segs[blockIdx.x];
-    const CloudDev C = cd[s.cloud];
-    const int j = s.start + threadIdx.x;
-    if (j < C.n) C.nstate[j] = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2265,6 +1987,85 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
 
 }  // namespace
 
+#ifdef LSM_DIAG
+// diagnostics builds: phase statistics of the one-kernel form to stderr (LSM_NORMALS_PHASES)
+int normals_phases(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
+                   const NormalParams &np, int64_t npts) {
+    hipStream_t st = ctx->stream;
+    unsigned long long *d_ph = (unsigned long long *)ctx->buf("n_phase", 16 * 8);
+    if (!d_ph) return LSM_ENOMEM;
+    LSM_HIP_TRY(ctx, hipMemsetAsync(d_ph, 0, 16 * 8, st));
+    normals_phase_kernel<<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_ph);
+    unsigned long long h[16];
+    LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ph, sizeof(h), hipMemcpyDeviceToHost, st));
+    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+    const char *nm[8] = {"s1_steps", "s1_members", "refine_steps", "final_steps",
+                         "final_added", "dense", "refines", "pred_dense"};
+    fprintf(stderr, "normals phases over %lld points (lane sum / point, wave max sum / point):\n",
+            (long long)npts);
+    for (int c = 0; c < 8; ++c)
+        fprintf(stderr, "  %-13s %10.3f %10.3f\n", nm[c], double(h[c]) / double(npts),
+                double(h[8 + c]) * 64.0 / double(npts));
+    return LSM_OK;
+}
+#endif
+
+// Every normal of the clouds of `d_segs` (one workgroup per 256-point segment; K clouds, N >= the
+// batch's points, d_geo: each cloud's pt_off into the batch lists, npts: the points):
+//   * the split launch -- the sparse half (the points predicted sparse: scan 1 with cumulants and
+//     count, finished when the ball holds <= max_nn), the deferred points in full waves of the
+//     clouds' dense lists, and the few the dense half leaves to a refine scan -- or, with
+//     LSM_NORMALS_SPLIT=0 (a test knob: bit-identical), the one-kernel form;
+//   * then the small-neighbourhood pass (Open3D's covariance arithmetic, normals_small_kernel).
+// In statistics mode (lsm_set_timing(ctx, 2)) it also counts the neighbours of every normal
+// (SURVEY.md §8d's algorithmic work) and the points that needed the kNN truncation.
+int run_normals(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
+                const GridGeo *d_geo, int K, size_t N, const NormalParams &np, int64_t npts) {
+    if (nseg <= 0) return LSM_OK;
+    hipStream_t st = ctx->stream;
+    unsigned long long *d_ns = nullptr;
+    if (ctx->statistics) {
+        d_ns = (unsigned long long *)ctx->buf("n_stats", 72 * 8);
+        if (!d_ns) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 72 * 8, st));
+    }
+#ifdef LSM_DIAG
+    if (getenv("LSM_NORMALS_PHASES")) {
+        const int rc = normals_phases(ctx, d_segs, nseg, d_cd, np, npts);
+        if (rc) return rc;
+    }
+#endif
+    if (lsm_knob("LSM_NORMALS_SPLIT", 1.0) != 0.0) {
+        uint32_t *dlist = (uint32_t *)ctx->buf("n_dlist", N * 4);
+        uint32_t *dcnt = (uint32_t *)ctx->buf("n_dcnt", size_t(K) * 8);
+        uint32_t *rlist = (uint32_t *)ctx->buf("n_rlist", N * 4);
+        if (!dlist || !dcnt || !rlist) return LSM_ENOMEM;
+        LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, size_t(K) * 8, st));
+        normals_sparse_kernel<NORMALS_G_DEFAULT><<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, d_geo,
+                                                                             np, dlist, dcnt, d_ns);
+        launch_dense_half<NORMALS_GD_DEFAULT>(st, d_segs, nseg, d_cd, d_geo, K, np, dlist, dcnt,
+                                              d_ns, rlist, dcnt + K);
+    } else {
+        normals_kernel<NORMALS_G_DEFAULT><<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_ns);
+    }
+    // (the grid's sort keys are dead by now: their buffer holds the small-neighbourhood list)
+    uint2 *slist = (uint2 *)ctx->buf("g_kin", N * 8);
+    uint32_t *scnt = (uint32_t *)ctx->buf("n_small_n", 4);
+    if (!slist || !scnt) return LSM_ENOMEM;
+    launch_small_normals(st, d_segs, nseg, d_cd, np, slist, scnt, ctx->num_cus);
+    if (d_ns) {
+        unsigned long long h[72] = {};
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ns, sizeof(h), hipMemcpyDeviceToHost, st));
+        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+        ctx->stats["normals_truncated"].launches += int64_t(h[0]);
+        unsigned long long nb = 0;
+        for (int k = 8; k < 72; ++k) nb += h[k];
+        ctx->stats["normals_neighbours"].launches += int64_t(nb);
+        ctx->stats["normals_points"].launches += npts;
+    }
+    return LSM_OK;
+}
+
 int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params &p,
                    int64_t *n_out) {
     hipStream_t st = ctx->stream;
@@ -2330,15 +2131,6 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     for (int k = 0; k < K; ++k) {
         Cloud *c = clouds[k];
         if ((rc = ensure_cloud_buffers(ctx, c, wn[k], p.want_normals != 0))) return rc;
-        if (p.want_normals == LSM_NORMALS_LAZY && (c->nstate_cap < int64_t(wn[k]) || !c->d_nstate)) {
-            (void)hipFree(c->d_nstate);
-            c->d_nstate = nullptr;
-            c->nstate_cap = std::max<int64_t>(int64_t(wn[k]), 1);
-            if (hipMalloc(&c->d_nstate, size_t(c->nstate_cap)) != hipSuccess) {
-                ctx->set_error("hipMalloc failed (lazy normal states)");
-                return LSM_ENOMEM;
-            }
-        }
         const int64_t ncells = int64_t(geo[k].ncells);
         if (c->cell_cap < ncells + 1 || !c->d_cell) {
             (void)hipFree(c->d_cell);
@@ -2431,111 +2223,12 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
 
     // ---------------- normals ----------------
     const bool lazy = p.want_normals == LSM_NORMALS_LAZY;
-    if (lazy && !psegs.empty()) {   // normals on demand: every point pending
-        std::vector<CloudDev> zc(cdev);
-        for (int k = 0; k < K; ++k) zc[k].nstate = clouds[k]->d_nstate;
-        CloudDev *d_zc;
-        if ((rc = upload_vec(ctx, "g_cdz", zc, &d_zc))) return rc;
-        nstate_zero_kernel<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_zc);
-    }
     if (p.want_normals && !lazy && !psegs.empty()) {
         const NormalParams np = normal_params(p.normal_radius, p.max_nn);
+        int64_t npts = 0;
+        for (int k = 0; k < K; ++k) npts += wn[k];
         ctx->tic("normals", &ev);
-        {
-            // LSM_NORMALS_STATS (read per call): count the points that needed the kNN
-            // truncation and the neighbours of every normal (slower: statistics runs only)
-            const bool nstats = getenv("LSM_NORMALS_STATS") != nullptr;
-            unsigned long long *d_ns = nullptr;
-            if (nstats) {
-                d_ns = (unsigned long long *)ctx->buf("n_stats", 72 * 8);
-                if (!d_ns) return LSM_ENOMEM;
-                LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 72 * 8, st));
-            }
-            static const int G = [] {   // LSM_NORMALS_G: points per load group of the walks
-                const char *e = getenv("LSM_NORMALS_G");
-                return e ? atoi(e) : NORMALS_G_DEFAULT;
-            }();
-            const dim3 ng(unsigned(psegs.size()));
-            if (getenv("LSM_NORMALS_PHASES")) {   // diagnostics: phase statistics to stderr
-                unsigned long long *d_ph = (unsigned long long *)ctx->buf("n_phase", 16 * 8);
-                if (!d_ph) return LSM_ENOMEM;
-                LSM_HIP_TRY(ctx, hipMemsetAsync(d_ph, 0, 16 * 8, st));
-                normals_phase_kernel<<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, np, d_ph);
-                unsigned long long h[16];
-                LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ph, sizeof(h), hipMemcpyDeviceToHost, st));
-                LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-                int64_t npts = 0;
-                for (int k = 0; k < K; ++k) npts += wn[k];
-                const char *nm[8] = {"s1_steps", "s1_members", "refine_steps", "final_steps",
-                                     "final_added", "dense", "refines", "pred_dense"};
-                fprintf(stderr, "normals phases over %lld points (lane sum / point, wave max sum / point):\n",
-                        (long long)npts);
-                for (int c = 0; c < 8; ++c)
-                    fprintf(stderr, "  %-13s %10.3f %10.3f\n", nm[c], double(h[c]) / double(npts),
-                            double(h[8 + c]) * 64.0 / double(npts));
-            }
-            // LSM_NORMALS_XLDS=<bytes> (diagnostics, read per call): extra dynamic LDS per
-            // workgroup, lowering the kernel's occupancy (the occupancy-sensitivity probe)
-            const char *xl = getenv("LSM_NORMALS_XLDS");
-            const size_t xlds = xl ? size_t(atol(xl)) : 0;
-            // LSM_NORMALS_SPLIT (read per call; default on): the two-kernel launch
-            const char *sp = getenv("LSM_NORMALS_SPLIT");
-            const bool split = !sp || atoi(sp) != 0;
-            if (split) {
-                uint32_t *dlist = (uint32_t *)ctx->buf("n_dlist", N * 4);
-                uint32_t *dcnt = (uint32_t *)ctx->buf("n_dcnt", size_t(K) * 8);
-                uint32_t *rlist = (uint32_t *)ctx->buf("n_rlist", N * 4);
-                if (!dlist || !dcnt || !rlist) return LSM_ENOMEM;
-                uint32_t *rcnt = dcnt + K;   // the refine lists' counts
-                LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, size_t(K) * 8, st));
-                // LSM_NORMALS_GD: points per load group of the dense half (its occupancy is
-                // set by the LDS rows, so it has registers to spare for wider groups)
-                static const int GD = [] {
-                    const char *e = getenv("LSM_NORMALS_GD");
-                    return e ? atoi(e) : NORMALS_GD_DEFAULT;
-                }();
-                const char *cl = getenv("LSM_NORMALS_CLASSIFY");   // read per call
-                if (cl && atoi(cl) != 0) {
-                    uint32_t *slist = (uint32_t *)ctx->buf("n_slist", N * 4);
-                    uint32_t *scnt = (uint32_t *)ctx->buf("n_scnt", size_t(K) * 4);
-                    if (!slist || !scnt) return LSM_ENOMEM;
-                    LSM_HIP_TRY(ctx, hipMemsetAsync(scnt, 0, size_t(K) * 4, st));
-                    normals_classify_kernel<<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, slist, scnt, dlist, dcnt);
-                    normals_sparse_kernel<2, true><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns, slist, scnt);
-                } else if (G == 4)
-                    normals_sparse_kernel<4><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
-                else
-                    normals_sparse_kernel<2><<<ng, PT_THREADS, 0, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
-                const char *co = getenv("LSM_NORMALS_COOP");   // read per call
-                const bool coop = co && atoi(co) != 0;
-                if (coop)
-                    normals_dense_coop_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, d_geo, np, dlist, dcnt, d_ns);
-                else if (GD == 8)
-                    launch_dense_half<8>(st, d_psegs, int(psegs.size()), d_cd, d_geo, K, np, dlist, dcnt, d_ns, rlist, rcnt, xlds);
-                else if (GD == 4)
-                    launch_dense_half<4>(st, d_psegs, int(psegs.size()), d_cd, d_geo, K, np, dlist, dcnt, d_ns, rlist, rcnt, xlds);
-                else if (GD == 3)
-                    launch_dense_half<3>(st, d_psegs, int(psegs.size()), d_cd, d_geo, K, np, dlist, dcnt, d_ns, rlist, rcnt, xlds);
-                else
-                    launch_dense_half<2>(st, d_psegs, int(psegs.size()), d_cd, d_geo, K, np, dlist, dcnt, d_ns, rlist, rcnt, xlds);
-            } else if (G == 1) normals_kernel<1><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
-            else if (G == 2) normals_kernel<2><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
-            else if (G == 8) normals_kernel<8><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
-            else normals_kernel<4><<<ng, PT_THREADS, xlds, st>>>(d_psegs, d_cd, np, d_ns);
-            if (nstats) {
-                unsigned long long h[72] = {};
-                LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ns, sizeof(h), hipMemcpyDeviceToHost, st));
-                LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-                ctx->stats["normals_truncated"].launches += int64_t(h[0]);
-                unsigned long long nb = 0;
-                for (int k = 8; k < 72; ++k) nb += h[k];
-                KStat &ns = ctx->stats["normals_neighbours"];
-                ns.launches += int64_t(nb);
-                int64_t npts = 0;
-                for (int k = 0; k < K; ++k) npts += wn[k];
-                ctx->stats["normals_points"].launches += npts;
-            }
-        }
+        if ((rc = run_normals(ctx, d_psegs, int(psegs.size()), d_cd, d_geo, K, N, np, npts))) return rc;
         ctx->toc("normals", ev);
     }
 
@@ -2560,71 +2253,13 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     return LSM_OK;
 }
 
-int lsm_normals_lazy_pass(lsm_ctx *ctx, const LazyNormals &lz, const CloudDev *cds, int pass) {
-    if (lz.tb <= 0 || lz.nl <= 0) return LSM_OK;
-    hipStream_t st = ctx->stream;
-    hipEvent_t ev;
-    uint32_t *cnt = lz.counters + 2 * pass;                 // [0] listed blocks, [1] waves
-    uint32_t *ccnt = lz.cloud_cnt + size_t(pass) * lz.nl;   // gathered points per cloud
-    uint32_t *woff = lz.woff + size_t(pass) * (lz.nl + 1);
-    ctx->tic("normals_mark", &ev);
-    lazy_compact_kernel<<<(lz.tb + 255) / 256, 256, 0, st>>>(lz.blkflag, lz.tb, lz.list, cnt);
-    lazy_gather_kernel<<<std::max(1, ctx->num_cus * 8), 256, 0, st>>>(
-        cds, lz.tb_off, lz.lazy_cd, lz.pt_off, lz.nl, lz.list, cnt, ccnt, lz.plist);
-    lazy_waves_kernel<<<1, 1024, 0, st>>>(ccnt, lz.nl, woff, cnt);
-    ctx->toc("normals_mark", ev);
-    // the waves' count decides the grid: one small read-back per pass (the kernels queued so
-    // far drain meanwhile; ~10-20 us against ~90 ms of ICP per step)
-    LSM_HIP_TRY(ctx, hipMemcpyAsync(lz.host_count, cnt + 1, 4, hipMemcpyDeviceToHost, st));
-    LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-    const uint32_t nw = *lz.host_count;
-    if (nw == 0) return LSM_OK;
-    const NormalParams np = normal_params(lz.radius, lz.max_nn);
-    // LSM_NORMALS_STATS (read per call): neighbourhood sizes of the normals computed
-    unsigned long long *d_ns = nullptr;
-    if (getenv("LSM_NORMALS_STATS")) {
-        d_ns = (unsigned long long *)ctx->buf("lz_stats", 72 * 8);
-        if (!d_ns) return LSM_ENOMEM;
-        LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 72 * 8, st));
-    }
-    const int wpg = PT_THREADS / LSM_WAVE;
-    ctx->tic("normals_lazy", &ev);
-    lazy_normals_kernel<<<(nw + wpg - 1) / wpg, PT_THREADS, 0, st>>>(
-        cds, lz.lazy_cd, lz.pt_off, lz.nl, np, woff, ccnt, lz.plist, d_ns);
-    ctx->toc("normals_lazy", ev);
-    ctx->stats["normals_lazy_waves"].launches += int64_t(nw);
-    if (getenv("LSM_DEBUG_LAZY")) {   // per pass: waves and kernel time (synchronous)
-        hipEvent_t a = ctx->get_event(), b = ctx->get_event();
-        LSM_HIP_TRY(ctx, hipEventRecord(a, st));
-        lazy_normals_kernel<<<(nw + wpg - 1) / wpg, PT_THREADS, 0, st>>>(
-            cds, lz.lazy_cd, lz.pt_off, lz.nl, np, woff, ccnt, lz.plist, nullptr);
-        LSM_HIP_TRY(ctx, hipEventRecord(b, st));
-        LSM_HIP_TRY(ctx, hipEventSynchronize(b));
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, a, b);
-        fprintf(stderr, "lazy pass %2d: waves %8u  (re-run) %.3f ms\n", pass, nw, ms);
-        ctx->event_pool.push_back(a);
-        ctx->event_pool.push_back(b);
-    }
-    if (d_ns) {
-        unsigned long long h[72] = {};
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ns, sizeof(h), hipMemcpyDeviceToHost, st));
-        LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
-        unsigned long long nbr = 0;
-        for (int k = 8; k < 72; ++k) nbr += h[k];
-        ctx->stats["normals_neighbours"].launches += int64_t(nbr);
-        ctx->stats["normals_points"].launches += int64_t(h[1]);
-    }
-    return LSM_OK;
-}
-
 int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
     hipStream_t st = ctx->stream;
     int rc;
     // one pass per (radius, max_nn) of the pending clouds
     std::vector<Cloud *> todo;
     for (Cloud *c : clouds)
-        if (c && c->lazy && c->n > 0 && c->d_nstate && c->d_nrm) todo.push_back(c);
+        if (c && c->lazy && c->n > 0 && c->d_nrm) todo.push_back(c);
     while (!todo.empty()) {
         const double r = todo[0]->lazy_radius;
         const int mnn = todo[0]->lazy_max_nn;
@@ -2632,78 +2267,32 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
         for (Cloud *c : todo) (c->lazy_radius == r && c->lazy_max_nn == mnn ? grp : rest).push_back(c);
         std::vector<CloudDev> cd(grp.size());
         std::vector<uint32_t> n(grp.size());
+        std::vector<GridGeo> gg(grp.size());
+        uint32_t tot = 0;
         for (size_t k = 0; k < grp.size(); ++k) {
             cd[k] = grp[k]->dev;
             cd[k].nrm = grp[k]->d_nrm;
-            cd[k].nstate = grp[k]->d_nstate;
             n[k] = uint32_t(grp[k]->n);
+            gg[k] = GridGeo{};
+            gg[k].pt_off = tot;
+            gg[k].n = n[k];
+            tot += n[k];
         }
         std::vector<Seg> segs = point_segments(n, PT_THREADS);
         CloudDev *d_cd;
         Seg *d_segs;
+        GridGeo *d_gg;
         if ((rc = upload_vec(ctx, "lz_cd", cd, &d_cd))) return rc;
         if ((rc = upload_vec(ctx, "lz_segs", segs, &d_segs))) return rc;
-        // LSM_NORMALS_STATS (read per call): neighbourhood sizes of the normals computed
-        unsigned long long *d_ns = nullptr;
-        if (getenv("LSM_NORMALS_STATS")) {
-            d_ns = (unsigned long long *)ctx->buf("lz_stats", 72 * 8);
-            if (!d_ns) return LSM_ENOMEM;
-            LSM_HIP_TRY(ctx, hipMemsetAsync(d_ns, 0, 72 * 8, st));
-        }
-        // the eager path's split launch (sparse half, then the deferred points in full waves;
-        // bit-identical to the one-kernel form, points already computed are skipped) unless
-        // LSM_NORMALS_SPLIT=0 (read per call): one complete_normals_kernel over the pending points
-        const char *sp = getenv("LSM_NORMALS_SPLIT");
-        const bool split = !sp || atoi(sp) != 0;
-        GridGeo *d_gg = nullptr;
-        uint32_t *dlist = nullptr, *dcnt = nullptr, *rlist = nullptr;
-        if (split && !segs.empty()) {
-            std::vector<GridGeo> gg(grp.size());
-            uint32_t tot = 0;
-            for (size_t k = 0; k < grp.size(); ++k) {
-                gg[k] = GridGeo{};
-                gg[k].pt_off = tot;
-                gg[k].n = n[k];
-                tot += n[k];
-            }
-            if ((rc = upload_vec(ctx, "lz_gg", gg, &d_gg))) return rc;
-            dlist = (uint32_t *)ctx->buf("lz_dlist", size_t(tot) * 4);
-            dcnt = (uint32_t *)ctx->buf("lz_dcnt", grp.size() * 8);
-            rlist = (uint32_t *)ctx->buf("lz_rlist", size_t(tot) * 4);
-            if (!dlist || !dcnt || !rlist) return LSM_ENOMEM;
-            LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, grp.size() * 8, st));
-        }
+        if ((rc = upload_vec(ctx, "lz_gg", gg, &d_gg))) return rc;
         hipEvent_t ev;
         ctx->tic("normals_lazy", &ev);
-        if (!segs.empty()) {
-            const NormalParams np = normal_params(r, mnn);
-            if (split) {
-                normals_sparse_kernel<2><<<int(segs.size()), PT_THREADS, 0, st>>>(
-                    d_segs, d_cd, d_gg, np, dlist, dcnt, d_ns);
-                launch_dense_half<2>(st, d_segs, int(segs.size()), d_cd, d_gg, int(grp.size()), np,
-                                     dlist, dcnt, d_ns, rlist, dcnt + grp.size(), 0);
-            } else {
-                complete_normals_kernel<<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_ns);
-            }
-        }
+        if ((rc = run_normals(ctx, d_segs, int(segs.size()), d_cd, d_gg, int(grp.size()),
+                              std::max<size_t>(tot, 1), normal_params(r, mnn), int64_t(tot))))
+            return rc;
         ctx->toc("normals_lazy", ev);
         LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
         LSM_HIP_TRY(ctx, hipGetLastError());
-        if (d_ns) {
-            unsigned long long h[72] = {};
-            LSM_HIP_TRY(ctx, hipMemcpy(h, d_ns, sizeof(h), hipMemcpyDeviceToHost));
-            unsigned long long nbr = 0;
-            for (int k = 8; k < 72; ++k) nbr += h[k];
-            ctx->stats["normals_neighbours"].launches += int64_t(nbr);
-            if (split) {   // (the split kernels count no points: the pending ones, all of them
-                           // unless an earlier per-point batch computed some)
-                int64_t np_ = 0;
-                for (uint32_t v : n) np_ += v;
-                ctx->stats["normals_points"].launches += np_;
-            } else {
-                ctx->stats["normals_points"].launches += int64_t(h[1]);
-            }
-        }
         for (Cloud *c : grp) c->lazy = false;
         todo.swap(rest);
     }

@@ -627,8 +627,9 @@ int lsmcpu_normals(const double *xyz, int64_t n, double radius, int max_nn, doub
                     s[7] += p[1] * p[2];
                     s[8] += p[2] * p[2];
                 }
-                const double inv = 1.0 / double(c);
-                for (double &v : s) v *= inv;
+                // Eigen's `cumulants /= n` divides each cumulant (no reciprocal)
+                const double dn = double(c);
+                for (double &v : s) v /= dn;
                 C[0] = s[3] - s[0] * s[0];
                 C[1] = s[4] - s[0] * s[1];
                 C[2] = s[5] - s[0] * s[2];

@@ -271,22 +271,28 @@ def fast_eigen3x3(covs):
 
 
 def estimate_normals(points, radius=NORMAL_RADIUS, max_nn=MAX_NN, chunk=4096,
-                     return_counts=False):
-    """EstimateNormals with no prior normals: cov per point, FastEigen3x3, zero -> (0,0,1)."""
+                     return_counts=False, return_covs=False):
+    """EstimateNormals with no prior normals: cov per point, FastEigen3x3, zero -> (0,0,1).
+
+    return_counts / return_covs add the neighbourhood sizes / the covariances to the result."""
     p = np.asarray(points, dtype=np.float64)
     tree = cKDTree(p)
     normals = np.empty_like(p)
     counts = np.empty(len(p), dtype=np.int64)
+    all_covs = np.empty((len(p), 3, 3)) if return_covs else None
     for a in range(0, len(p), chunk):
         q = p[a:a + chunk]
         idx, _, cnt = hybrid_search(tree, p, q, radius, max_nn)
         covs = compute_covariance(p, idx, cnt)
+        if return_covs:
+            all_covs[a:a + chunk] = covs
         counts[a:a + chunk] = cnt
         n = fast_eigen3x3(covs)
         zero = np.sqrt(_dot(n, n)) == 0.0
         n[zero] = (0.0, 0.0, 1.0)
         normals[a:a + chunk] = n
-    return (normals, counts) if return_counts else normals
+    out = (normals,) + ((counts,) if return_counts else ()) + ((all_covs,) if return_covs else ())
+    return out if len(out) > 1 else normals
 
 
 # --------------------------------------------------------------------------------------------

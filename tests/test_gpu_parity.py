@@ -129,9 +129,8 @@ def test_normals_preclassification_bit_identical(dev, seq64k, max_nn, monkeypatc
 @pytest.mark.parametrize("max_nn", [300, 30])
 def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
     """The split launch (default: the points predicted sparse, then every deferred point in
-    full waves of the clouds' dense lists; its dense half with per-lane walks or with the
-    wave-cooperative scans, LSM_NORMALS_COOP; its sparse half over a pre-classified list,
-    LSM_NORMALS_CLASSIFY) against the one-kernel launch (LSM_NORMALS_SPLIT=0):
+    full waves of the clouds' dense lists, then the rare refine scans) against the one-kernel
+    launch (LSM_NORMALS_SPLIT=0):
     bit-identical normals on bench scans, under heavier truncation, on degenerate neighbourhoods
     (duplicates saturating a u8 bin, a dense patch) and on clouds that carry prior normals
     (EstimateNormals re-run on a cloud with normals orients to them)."""
@@ -144,24 +143,20 @@ def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
     keep = _lib.prep_params(max_nn=max_nn, min_radius=-np.inf, max_radius=1e15,
                             min_height=-1e15, max_height=1e15)
     out = {}
-    for split, coop, cls in (("1", "0", "0"), ("1", "1", "0"), ("1", "0", "1"), ("0", "0", "0")):
+    for split in ("1", "0"):
         monkeypatch.setenv("LSM_NORMALS_SPLIT", split)
-        monkeypatch.setenv("LSM_NORMALS_COOP", coop)
-        monkeypatch.setenv("LSM_NORMALS_CLASSIFY", cls)
         ids = [dev.upload(c) for c in clouds]
         try:
             dev.preprocess(ids, prm)
             first = [dev.download(i, normals=True)[1] for i in ids]
             dev.preprocess(ids, keep)          # again, now with prior normals
             second = [dev.download(i, normals=True)[1] for i in ids]
-            out[split + coop + cls] = first + second
+            out[split] = first + second
         finally:
             _release(dev, ids)
-    for v in ("LSM_NORMALS_SPLIT", "LSM_NORMALS_COOP", "LSM_NORMALS_CLASSIFY"):
-        monkeypatch.delenv(v)
-    for variant in ("100", "110", "101"):
-        for a, b in zip(out[variant], out["000"]):
-            assert np.array_equal(a, b), variant
+    monkeypatch.delenv("LSM_NORMALS_SPLIT")
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("voxel", [0.0, 0.1])
@@ -426,8 +421,7 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monk
         _release(dev, ids)
 
 
-@pytest.mark.parametrize("env", [{"LSM_NN_FB": "64"}, {"LSM_NN_FB": "16"},
-                                 {"LSM_NN_FB_FAR": "0.75"}, {"LSM_NN_CERT_FROM": "1"},
+@pytest.mark.parametrize("env", [{"LSM_NN_CERT_FROM": "1"},
                                  {"LSM_NN_CERT_FROM": "4"}, {"LSM_NN_DIRECT": "0"},
                                  {"LSM_NN_DIRECT": "1", "LSM_NN_DIRECT_ITER": "0"},
                                  {"LSM_NN_DIRECT": "2.5", "LSM_NN_DIRECT_ITER": "1"},
@@ -436,8 +430,8 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monk
                                  {"LSM_NN_SPLIT_PLACE": "1"}, {"LSM_NN_SPLIT_PLACE": "2"},
                                  {"LSM_NN_NOCERT": "1"}])
 def test_search_path_variants_bit_identical(dev, env, monkeypatch):
-    """The exact 1-NN may be reached along different paths: fallback groups of 16 / 32 / 64
-    lanes, the near/far fallback split, the stability check from pass 1, 2 or 4, queries with a
+    """The exact 1-NN may be reached along different paths: the stability check from pass 1, 2
+    or 4, queries with a
     far warm start sent straight to the fallback (from 1 cell in every pass, from 2.5 cells
     after the first update, the default 3 cells after 12 updates, or never), cold-start boxes
     of 3^3 / 5^3 / 9^3 (default) / 13^3 cells, warm boxes capped at 2 / 3 / 4 (default) cells,
@@ -578,15 +572,12 @@ def _assert_batch_equal(a, b):
         assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
 
 
-@pytest.mark.parametrize("per_point", [False, True])
-def test_lazy_normals_bit_identical_on_bench_sequence(dev, per_point, monkeypatch):
-    """LSM_NORMALS_LAZY (bench.py's default): each target normal is computed when a
-    correspondence first reaches it. The registrations, their correspondence sets and -- once
-    completed by the download -- every normal equal the eager pre-process bit for bit (seed-3
-    sequence, 24 pairs including non-converging ones); a second batch on the same clouds reuses
-    the computed normals and still agrees."""
-    if per_point:
-        monkeypatch.setenv("LSM_NORMALS_LAZY_POINTS", "1")
+def test_lazy_normals_bit_identical_on_bench_sequence(dev):
+    """LSM_NORMALS_LAZY (bench.py's C4 / C5 mode): a keyframe's normals are computed when it is
+    first a P2Plane target. The registrations, their correspondence sets and -- once completed
+    by the download -- every normal equal the eager pre-process bit for bit (seed-3 sequence, 24
+    pairs including non-converging ones); a second batch on the same clouds reuses the computed
+    normals and still agrees."""
     seq = synthetic.make_sequence(25, seed=3, model=synthetic.HDL64)
     icp = _lib.icp_params()
     eager = _prep(dev, seq.scans)
@@ -601,10 +592,6 @@ def test_lazy_normals_bit_identical_on_bench_sequence(dev, per_point, monkeypatc
         c_got = dev.last_correspondences()
         _assert_batch_equal(ref, got)
         assert np.array_equal(c_ref, c_got)
-        if per_point:   # only the reached normals, pass by pass
-            waves = dev.kernel_stats("normals_lazy_waves")["launches"]
-            npts = sum(dev.info(h)[1] for h in lazy[:-1])
-            assert 0 < 64 * waves < 1.5 * npts
         again = dev.icp_batch_arrays(lazy[1:], lazy[:-1], seq.priors, icp)
         _assert_batch_equal(ref, again)
         for e, l in zip(eager, lazy):
@@ -615,16 +602,10 @@ def test_lazy_normals_bit_identical_on_bench_sequence(dev, per_point, monkeypatc
         _release(dev, eager + lazy)
 
 
-def test_lazy_normals_revisit_pairs_and_p2p(dev, monkeypatch):
-    """C4-style revisit pairs (large initial errors: many fallback queries, which mark their
-    targets too) with lazy targets and lazy sources whose normals are never needed; P2P on lazy
-    clouds (no normals read); a batch mixing eager and lazy targets. All equal the eager runs."""
-    for per_point in ("0", "1"):
-        monkeypatch.setenv("LSM_NORMALS_LAZY_POINTS", per_point)
-        _lazy_revisit(dev)
-
-
-def _lazy_revisit(dev):
+def test_lazy_normals_revisit_pairs_and_p2p(dev):
+    """C4-style revisit pairs (large initial errors: many fallback queries) with lazy targets and
+    lazy sources whose normals are never needed; P2P on lazy clouds (no normals read); a batch
+    mixing eager and lazy targets. All equal the eager runs."""
     ps = synthetic.make_revisit_pairs(4, seed=41, model=synthetic.HDL64)
     scans = ps.targets + ps.sources
     eager = _prep(dev, scans)
