@@ -14,8 +14,8 @@ Prints one JSON line (rank 0) with the roofline of the NN correspondence kernel 
 the library's own stream, SURVEY.md §8d algorithmic bytes), the roofline of the normals kernel
 (VALU issue from the committed PMC instruction count, and algorithmic FLOPs from the device's
 neighbourhood sizes), a CPU baseline (the C++/OpenMP f64 implementation under oracle/cpu, rank 0
-at N = 1 only, bounded sample, every usable core and 1 core) and config C1's line (8k-point P2P
-pairs: the CPU implementation, and the same pairs on the GPU).
+at N = 1 only, bounded sample, every usable core and 1 core) and the lines of configs C1 (8k-point
+P2P pairs) and C2 (one 64k P2Plane pair): the CPU implementation, and the same pairs on the GPU.
 """
 from __future__ import annotations
 
@@ -36,8 +36,40 @@ FP32_VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md chip-level parameters (vec
 # VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one 64-lane wave instruction per 2 cycles per
 # SIMD (MI355X_MICROARCH.md 'Wave scheduling'), in G wave-instructions/s
 VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 2   # = 1228.8
-KERNELS = ["filter", "grid", "normals", "normals_lazy", "normals_mark", "nn", "nn_fallback",
-           "accumulate", "solve", "voxel"]
+KERNELS = ["filter", "grid", "normals", "normals_lazy", "nn", "nn_fallback", "accumulate",
+           "solve", "voxel"]
+
+
+def source_sha() -> str:
+    """SHA-256 of the library's sources (lidar_slam_arvc_amd/csrc, include/lidarsm.h): the PMC
+    counts committed under profiles/ carry the hash of the build they were counted on, and the
+    bench line uses them only while it matches."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "lidar_slam_arvc_amd", "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")))
+    for f in [os.path.join(csrc, f) for f in files] + [os.path.join(ROOT, "include", "lidarsm.h")]:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def pmc_entry(name: str, workload: str, pairs: int, mode: str | None = None):
+    """The committed PMC summary of this workload (profiles/<name>, keyed by workload), or
+    (None, reason) when it is absent, of another size or mode, or counted on other sources."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None, "no PMC file"
+    with open(path) as f:
+        e = json.load(f).get(workload)
+    if not e:
+        return None, f"no PMC count for {workload}"
+    if e.get("pairs_per_gpu") != pairs or (mode is not None and e.get("normals_mode") != mode):
+        return None, "PMC count of another configuration"
+    if e.get("source_sha256") != source_sha():
+        return None, "stale: PMC counted on other library sources"
+    return e, None
 
 
 def parse():
@@ -80,25 +112,27 @@ def parse():
                     help="rehearse the multi-rank path on one GPU: all ranks on device 0, gloo "
                          "collectives on host tensors (tests only; not a scaling measurement)")
     ap.add_argument("--no-c1", action="store_true",
-                    help="skip config C1's line (8k-point P2P pairs, CPU and GPU)")
+                    help="skip the lines of configs C1 (8k-point P2P pairs) and C2 (one 64k "
+                         "P2Plane pair), CPU and GPU")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
     ap.add_argument("--seq-cache", default="",
-                    help="A/B runs (hdl64_seq): load the synthetic sequence from this .npz if it "
-                         "exists, else generate it and save it there")
+                    help="profiling / A/B runs: load the synthetic data from this .npz if it "
+                         "holds this workload's, else generate it and save it there")
     return ap.parse_args()
 
 
-def load_or_make_sequence(path, P, seed, model, first, procs):
+def load_or_make(path, tag, make):
+    """make() -> Sequence, or the one saved at `path` under the same tag (profiling runs: data
+    generation forks, which must not happen under the profiler, so a plain run fills the cache)."""
     from lidar_slam_arvc_amd import synthetic
-    tag = f"{P}_{seed}_{model.rings}x{model.azimuths}_{first}"
     if path and os.path.exists(path):
         z = np.load(path)
         if str(z["tag"]) == tag:
-            return synthetic.Sequence([z[f"s{k}"] for k in range(P + 1)], z["poses"], z["priors"])
-    seq = synthetic.make_sequence(P + 1, seed=seed, model=model, first_index=first,
-                                  processes=procs)
+            n = int(z["nscans"])
+            return synthetic.Sequence([z[f"s{k}"] for k in range(n)], z["poses"], z["priors"])
+    seq = make()
     if path:
-        np.savez(path, tag=tag, poses=seq.poses, priors=seq.priors,
+        np.savez(path, tag=tag, nscans=len(seq.scans), poses=seq.poses, priors=seq.priors,
                  **{f"s{k}": s for k, s in enumerate(seq.scans)})
     return seq
 
@@ -235,6 +269,48 @@ def c1_line(dev, seq, threads: int, cpu_pairs: int = 96):
             "unit": "pairs/s", "cpu_baseline": cpu}
 
 
+def c2_line(dev, seq, threads: int):
+    """Config C2 (BASELINE.json configs[1]): one 64k-point HDL-64 scan pair, point-to-plane ICP
+    on one GPU (keyframe.py:246-252 after pre_process of both keyframes, keyframe.py:113-124):
+    the seed-2 pair test_icp_parity checks against the oracle. GPU: per registration, with the
+    raw scans resident, pre-process both keyframes (filter + normals) and register the pair --
+    wall-clock latency per pair (mean over repeats) and its inverse; the kernel time split into
+    pre-process and ICP. CPU: the C++ implementation on the same pair."""
+    from lidar_slam_arvc_amd import _lib
+    ids = [dev.upload(s) for s in seq.scans]
+    prep = _lib.prep_params()
+    icp = _lib.icp_params()
+    try:
+        def run():
+            dev.preprocess(ids, prep)
+            return dev.icp_batch_arrays(ids[1:], ids[:1], seq.priors, icp)
+        for _ in range(3):
+            run()
+        dev.reset_stats()
+        dev.set_timing(True)
+        reps, t0 = 0, time.perf_counter()
+        while reps < 20 or time.perf_counter() - t0 < 1.0:
+            res = run()
+            reps += 1
+        dt = (time.perf_counter() - t0) / reps
+        dev.set_timing(False)
+        k_ms = {k: dev.kernel_stats(k)["ms"] / reps for k in KERNELS}
+    finally:
+        for h in ids:
+            dev.release(h)
+    cpu = cpu_baseline(seq, 1, "p2plane", threads,
+                       "the same seed-2 HDL-64 pair, P2Plane (both keyframes pre-processed)")
+    prep_ms = sum(k_ms[k] for k in ("filter", "grid", "normals", "voxel"))
+    icp_ms = sum(k_ms[k] for k in ("nn", "nn_fallback", "accumulate", "solve"))
+    return {"workload": "hdl64_64k_p2plane_pair (BASELINE.json configs[1]: one 64k-pt P2Plane "
+                        "pair, 1 GPU)",
+            "points_per_scan_post_filter": int(np.mean([len(s) for s in seq.scans])),
+            "gpu_ms_per_pair": round(dt * 1e3, 3), "gpu_value": round(1.0 / dt, 3),
+            "unit": "pairs/s", "icp_iterations": int(res["iterations"][0]),
+            "gpu_kernel_ms_per_pair": {"preprocess": round(prep_ms, 3), "icp": round(icp_ms, 3)},
+            "cpu_baseline": cpu, "cpu_ms_per_pair": round(1e3 / cpu["value"], 1)}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -253,20 +329,26 @@ def main():
     # synthetic scans first, in forked worker processes: nothing in this process has touched the
     # GPU yet (a fork after HIP initialisation is not safe)
     procs = max(1, min(8, os.cpu_count() or 1))
+    tag = f"{args.workload}_{P}_{seed}_{model.rings}x{model.azimuths}_{first}"
     if loop:
         # C4: every rank owns P independent revisit pairs (its own targets and sources)
-        ps = synthetic.make_revisit_pairs(P, seed=seed, model=model, first_index=first,
-                                          processes=procs)
-        seq = synthetic.Sequence(ps.targets + ps.sources, np.zeros((0, 4, 4)), ps.init)
-        del ps
+        def make():
+            ps = synthetic.make_revisit_pairs(P, seed=seed, model=model, first_index=first,
+                                              processes=procs)
+            return synthetic.Sequence(ps.targets + ps.sources, np.zeros((0, 4, 4)), ps.init)
     else:
-        seq = load_or_make_sequence(args.seq_cache, P, seed, model, first, procs)
-    c1 = None
+        def make():
+            return synthetic.make_sequence(P + 1, seed=seed, model=model, first_index=first,
+                                           processes=procs)
+    seq = load_or_make(args.seq_cache, tag, make)
+    c1 = c2 = None
     do_cpu = world == 1 and not args.no_cpu_baseline
     if do_cpu and not args.no_c1:
         # C1: 8k-point (16 x 512 ray) P2P pairs, seed 1 -- the reference's CPU-runnable case
         c1 = synthetic.make_sequence(C1_PAIRS + 1, seed=1, model=synthetic.VLP16_8K,
                                      processes=procs)
+        # C2: one 64k HDL-64 pair, seed 2
+        c2 = synthetic.make_sequence(2, seed=2, model=synthetic.HDL64, processes=procs)
     cpu_threads = args.cpu_threads or usable_cores()
 
     import torch
@@ -421,22 +503,22 @@ def main():
         step_s = norm_ms / args.steps * 1e-3
         flops = 18.0 * nb + 150.0 * npts
         valu, valu_k = None, None
-        vfile = os.path.join(ROOT, "profiles", "normals_valu.json")
-        if os.path.exists(vfile) and not (ouster or loop):
-            with open(vfile) as f:
-                vj = json.load(f)
-            # PMC count of the same workload and normals mode
-            if vj.get("pairs_per_gpu") == P and vj.get("normals_mode") == args.normals:
-                valu = vj.get("valu_per_step")
-                valu_k = {k: v.get("SQ_INSTS_VALU")
-                          for k, v in vj.get("per_kernel_per_step", {}).items()}
+        # PMC count of the same workload and normals mode (profiles/normals_valu.json)
+        vj, v_why = pmc_entry("normals_valu.json", args.workload, P, args.normals)
+        if vj:
+            valu = vj.get("valu_per_step")
+            valu_k = {k: v.get("SQ_INSTS_VALU")
+                      for k, v in vj.get("per_kernel_per_step", {}).items()}
         ach = valu / step_s / 1e9 if valu else None
-        roof_n = {"bound": "valu", "kernel": ("lazy_normals_kernel (the target normals each ICP "
-                                              "pass reaches)" if args.normals == "lazy" else
-                                              "normals_sparse_kernel + normals_dense_kernel "
-                                              "(the split launch, once per step)") +
-                                             ": hybrid kNN-300 / r 0.3 m",
+        roof_n = {"bound": "valu", "kernel": "normals_sparse_kernel + normals_dense_kernel + "
+                                             "normals_refine_kernel + normals_small_kernel (the "
+                                             "split launch; " +
+                                             ("each keyframe's normals when it is first a P2Plane "
+                                              "target" if args.normals == "lazy" else
+                                              "every keyframe, once per step") +
+                                             "): hybrid kNN-300 / r 0.3 m",
                   "mode": args.normals, "unit": "G wave-instructions/s",
+                  "valu_source": "profiles/normals_valu.json" if vj else v_why,
                   "achieved": round(ach, 2) if ach else None, "peak": VALU_ISSUE_PEAK_G,
                   "frac": round(ach / VALU_ISSUE_PEAK_G, 5) if ach else None,
                   "valu_instructions_per_step": valu,
@@ -459,16 +541,12 @@ def main():
     out = None
     if rank == 0:
         achieved = nn["algo_bytes"] / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0
-        traffic = None
-        tfile = os.path.join(ROOT, "profiles", "nn_traffic.json")
-        if os.path.exists(tfile) and not (ouster or loop):
-            with open(tfile) as f:
-                tj = json.load(f)
-            # PMC traffic of the same workload (profiles/nn_traffic.json, tools/pmc_nn.sh)
-            if tj.get("pairs_per_gpu") == P:
-                traffic = tj.get("hbm_bytes_per_launch")
+        # PMC traffic of the same workload (profiles/nn_traffic.json, tools/pmc_nn.sh)
+        tj, t_why = pmc_entry("nn_traffic.json", args.workload, P)
+        traffic = tj.get("hbm_bytes_per_launch") if tj else None
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "traffic_source": "profiles/nn_traffic.json" if tj else t_why,
                 "kernel": "correspondence pass: nn_kernel (stability check + box search) + "
                           "nn_fallback",
                 "algo_bytes_per_launch": nn["algo_bytes"] / max(nn["launches"], 1),
@@ -487,6 +565,7 @@ def main():
             else:
                 cpu = cpu_baseline(seq, ns, args.method, cpu_threads)
         c1_out = c1_line(dev, c1, cpu_threads) if c1 is not None else None
+        c2_out = c2_line(dev, c2, cpu_threads) if c2 is not None else None
         ms_step = dt / args.steps * 1e3
         out = {
             "metric": ("ICP keyframe-pair registrations/sec (256k-ray Ouster-128, multi-scale)"
@@ -530,6 +609,7 @@ def main():
             "roofline_normals": roof_n,
             "cpu_baseline": cpu,
             "c1": c1_out,
+            "c2": c2_out,
             "mean_icp_iterations": float(np.mean(iters)),
             "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
                                       for k, v in stats.items() if v["launches"]},

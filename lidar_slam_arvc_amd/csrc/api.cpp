@@ -621,7 +621,10 @@ int lsm_cloud_layout(lsm_ctx *ctx, lsm_cloud cloud, int32_t *perm, int64_t cap, 
     }
     const int64_t nc = int64_t(c->dev.nbx) * c->dev.nby * c->dev.nbz * LSM_BLK_CELLS;
     *ncells = nc;
-    if ((perm && cap < c->n) || (cells && cell_cap < nc + 1)) return LSM_EINVAL;
+    if ((perm && cap < c->n) || (cells && cell_cap < nc + 1)) {
+        ctx->set_error("perm / cells capacity too small");
+        return LSM_EINVAL;
+    }
     (void)hipSetDevice(ctx->device);
     if (perm && c->n > 0)
         LSM_HIP_TRY(ctx, hipMemcpyAsync(perm, c->d_perm, size_t(c->n) * 4, hipMemcpyDeviceToHost,

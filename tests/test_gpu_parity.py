@@ -86,21 +86,39 @@ def _normal_agreement(n_gpu, n_ref):
 
 @pytest.mark.parametrize("which", ["8k", "64k"])
 def test_normals(dev, seq8k, seq64k, which):
+    """Normals against both f64 oracles (keyframe.py:160-162). Every point whose covariance has
+    a separated spectrum (the two smallest eigenvalues apart by more than 1e-4 of the largest;
+    n >= 4 always is on these scans) agrees with the NumPy oracle to |n . n_ref| > 1 - 1e-6
+    (f32 storage of a unit normal: ~1e-7), truncated neighbourhoods included. The small
+    neighbourhoods (3 <= n <= 16, rank-deficient when their points are near-collinear) take
+    Open3D's own covariance arithmetic (normals_small_kernel) -- the C++ oracle's: their f32
+    normals equal its normals rounded to f32 bit for bit on >= 99.5 % of the points (the rest:
+    the device's and the host's acos / cos differ in the last bit), all within 1e-6, and the
+    three-point ones that differ are counted apart."""
+    from oracle import cpu_ref as C
     scan = (seq8k if which == "8k" else seq64k).scans[0]
     ids = _prep(dev, [scan])
     try:
         xyz, nrm = dev.download(ids[0], normals=True)
         ref_pts = O.filter_radius_height(scan)
         assert np.array_equal(xyz, ref_pts)
-        ref_n, counts = O.estimate_normals(ref_pts, return_counts=True)
+        ref_n, counts, covs = O.estimate_normals(ref_pts, return_counts=True, return_covs=True)
+        ev = np.linalg.eigvalsh(covs)
+        sep = (ev[:, 1] - ev[:, 0]) > 1e-4 * np.maximum(np.abs(ev[:, 2]), 1e-300)
         d = _normal_agreement(nrm, ref_n)
-        # f32 storage of the unit normal: |dot| = 1 to ~1e-7 where the spectrum is separated
-        good = d > 1.0 - 1e-5
-        assert good.mean() > 0.999, (good.mean(), np.sort(d)[:10])
-        # points whose neighbourhood was truncated to max_nn are covered
-        trunc = counts >= 300
-        if trunc.any():
-            assert good[trunc].mean() > 0.999
+        assert sep[counts >= 4].mean() > 0.999
+        assert (d[sep] > 1.0 - 1e-6).all(), np.sort(d[sep])[:10]
+        trunc = counts >= 300   # points whose neighbourhood was truncated to max_nn
+        assert (d[trunc & sep] > 1.0 - 1e-6).all()
+        c_n, c_cnt = C.estimate_normals(ref_pts, return_counts=True)
+        assert np.array_equal(c_cnt, counts)
+        small = (counts >= 3) & (counts <= 16)
+        g, f = nrm.astype(np.float32), c_n.astype(np.float32)
+        bit = np.all(g == f, axis=1) | np.all(g == -f, axis=1)
+        assert bit[small].mean() >= 0.995, bit[small].mean()
+        assert (_normal_agreement(nrm, c_n)[small] > 1.0 - 1e-6).all()
+        three = counts == 3
+        assert (~bit[three]).sum() <= max(2, 0.005 * three.sum()), (~bit[three]).sum()
     finally:
         _release(dev, ids)
 

@@ -11,7 +11,11 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_sha  # noqa: E402
+
 out = sys.argv[1]
+workload = sys.argv[2] if len(sys.argv) > 2 else "hdl64_seq"
 
 
 def total(counter):
@@ -38,9 +42,11 @@ for line in open(os.path.join(out, "FETCH_SIZE.log")):
 algo = bench["roofline"]["algo_bytes_per_launch"] if bench else None
 hbm = (2.0 * fetch_kb + write_kb) * 1024.0 / max(passes, 1)
 print(json.dumps({
+    "workload": workload,
+    "source_sha256": source_sha(),
     "kernel": "correspondence pass (nn_kernel + nn_fallback)",
     "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-              "bench.py --steps 2 --warmup 1, default workload (tools/pmc_nn.sh)",
+              f"bench.py --workload {workload} --steps 2 --warmup 1 (tools/pmc_nn.sh)",
     "passes": passes, "dispatches": [n1, n2],
     "pairs_per_gpu": bench["config"].get("pairs_per_gpu") if bench else None,
     "fetch_size_kb_per_pass": fetch_kb / max(passes, 1),

@@ -15,7 +15,11 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_sha  # noqa: E402
+
 out = sys.argv[1]
+workload = sys.argv[2] if len(sys.argv) > 2 else "hdl64_seq"
 bench = None
 for line in open(os.path.join(out, "sq.log")):
     if line.startswith("{"):
@@ -26,7 +30,8 @@ nsteps = (bench["steps"] + bench["warmup"] + 1) if bench else 1
 
 
 def kname(n):
-    m = re.search(r"normals_(sparse_kernel|dense_kernel|dense_coop_kernel|refine_kernel|kernel)", n)
+    m = re.search(r"normals_(sparse_kernel|dense_kernel|refine_kernel|small_list_kernel|"
+                  r"small_kernel|kernel)", n)
     return m.group(0) if m else n
 
 
@@ -55,10 +60,13 @@ for k, v in per.items():
 tot = sum(d.get("SQ_INSTS_VALU", 0.0) for d in kern.values())
 mode = bench["config"]["normals"].split(", ")[-1] if bench else None
 print(json.dumps({
-    "kernel": "every normals launch of a step (split launch: normals_sparse_kernel + normals_refine_kernel + "
-              "normals_dense_kernel; eager)",
-    "source": "rocprofv3 --kernel-trace --pmc SQ_* (two passes of 8), bench.py --steps 2 "
-              "--warmup 1, default workload (tools/pmc_normals_bench.sh)",
+    "workload": workload,
+    "source_sha256": source_sha(),
+    "kernel": "every normals launch of a step (split launch: normals_sparse_kernel + "
+              "normals_dense_kernel + normals_refine_kernel, then normals_small_list_kernel + "
+              "normals_small_kernel)",
+    "source": "rocprofv3 --kernel-trace --pmc SQ_* (two passes of 8), bench.py --workload "
+              f"{workload} --steps 2 --warmup 1 (tools/pmc_normals_bench.sh)",
     "steps_profiled": nsteps, "normals_mode": mode,
     "pairs_per_gpu": bench["config"].get("pairs_per_gpu") if bench else None,
     "per_kernel_per_step": kern,
