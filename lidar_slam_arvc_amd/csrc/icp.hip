@@ -51,6 +51,7 @@ struct NNParams {
     float direct_rc;   // warm-start distance (cells) from which a query skips the box search
     int direct_iter;   // ... once its pair has made this many updates
     int kcold, kmax;   // box half-widths (cells): cold start, largest warm box
+    int cold_seed;     // seed cold searches with a point of the query's own cell
 };
 
 // Correspondence state of one source point, carried from pass to pass (SoA arrays):
@@ -544,7 +545,17 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     const int cx = clampc(fx, G.nx), cy = clampc(fy, G.ny), cz = clampc(fz, G.nz);
     // box half-width in cells: the warm-start radius (+ f32 slack), else NN_KCOLD
     int K = prm.kcold;
-    if (t2.bd2 < INFINITY) {
+    if (t2.bidx < 0 && prm.cold_seed) {
+        // cold start: the middle point of the query's own cell (when it holds any) seeds the
+        // search, so the first rows' walks and x-ranges are pruned from the start; the box stays
+        // the cold one (NN_KCOLD), and the (d2, index) minimum does not depend on the seed
+        const int cl = lsm_cell_lin(G.nbx, G.nby, cx, cy, cz);
+        const uint32_t a = lsm_ld(G.cell_start, cl), b = lsm_ld(G.cell_start, cl + 1);
+        if (b > a) {
+            const int k = int((a + b) >> 1);
+            t2 = top3_init(k, sqd(lsm_ld(G.xyz, k), qx, qy, qz), m);
+        }
+    } else if (t2.bd2 < INFINITY) {
         const float rc = sqrtf(t2.bd2) * G.inv_cell * 1.0001f + 1e-4f;
         // In a pair that keeps iterating (direct_ok: >= NN_DIRECT_ITER updates, the chaotic
         // tail), a query whose previous neighbour lies >= NN_DIRECT_RC cells away needs a wide
@@ -1603,6 +1614,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         prm.direct_iter = int(lsm_knob("LSM_NN_DIRECT_ITER", NN_DIRECT_ITER));
         prm.kcold = std::max(1, int(lsm_knob("LSM_NN_KCOLD", NN_KCOLD)));
         prm.kmax = std::max(1, int(lsm_knob("LSM_NN_KMAX", NN_KMAX)));
+        prm.cold_seed = int(lsm_knob("LSM_NN_COLD_SEED", 1));
     }
 
     // Passes are launched back to back; the plan of each pass is rebuilt on the device after the

@@ -446,14 +446,15 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monk
                                  {"LSM_NN_KCOLD": "1"}, {"LSM_NN_KCOLD": "2"},
                                  {"LSM_NN_KMAX": "2"}, {"LSM_NN_KCOLD": "6", "LSM_NN_KMAX": "3"},
                                  {"LSM_NN_SPLIT_PLACE": "1"}, {"LSM_NN_SPLIT_PLACE": "2"},
-                                 {"LSM_NN_NOCERT": "1"}])
+                                 {"LSM_NN_NOCERT": "1"}, {"LSM_NN_COLD_SEED": "0"}])
 def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     """The exact 1-NN may be reached along different paths: the stability check from pass 1, 2
     or 4, queries with a
     far warm start sent straight to the fallback (from 1 cell in every pass, from 2.5 cells
     after the first update, the default 3 cells after 12 updates, or never), cold-start boxes
     of 3^3 / 5^3 / 9^3 (default) / 13^3 cells, warm boxes capped at 2 / 3 / 4 (default) cells,
-    split groups placed anywhere in the workgroup. Every choice
+    split groups placed anywhere in the workgroup, cold searches seeded with a point of the
+    query's own cell (default) or not. Every choice
     must give the same correspondences, so every result is bit-identical to the default's
     (C4-style revisit pairs: large initial errors, many fallback queries)."""
     ps = synthetic.make_revisit_pairs(6, seed=41, model=synthetic.HDL64)

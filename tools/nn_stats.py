@@ -1,5 +1,7 @@
 """Per-pass NN search statistics (LSM_NN_STATS, LSM_DEBUG_PASSES) on the first pairs of the
-bench's seed-3 sequence (diagnostics): python tools/nn_stats.py [P]"""
+bench's seed-3 sequence (diagnostics): python tools/nn_stats.py [P]
+(needs a diagnostics build: bash tools/build_ab.sh diag -DLSM_DIAG=1, run with LIDARSM_LIB=lidar_slam_arvc_amd/_lib/ab/diag.so)
+"""
 import os
 import sys
 

@@ -1,5 +1,7 @@
 """Normals phase statistics (LSM_NORMALS_PHASES): walk steps and members per phase of
-hybrid_lane on the first keyframes of the bench's seed-3 HDL-64 sequence (diagnostics)."""
+hybrid_lane on the first keyframes of the bench's seed-3 HDL-64 sequence (diagnostics).
+(needs a diagnostics build: bash tools/build_ab.sh diag -DLSM_DIAG=1, run with LIDARSM_LIB=lidar_slam_arvc_amd/_lib/ab/diag.so)
+"""
 import os
 import sys
 

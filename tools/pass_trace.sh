@@ -1,4 +1,5 @@
 #!/bin/bash
+# (needs a diagnostics build: bash tools/build_ab.sh diag -DLSM_DIAG=1, run with LIDARSM_LIB=lidar_slam_arvc_amd/_lib/ab/diag.so)
 # Per-pass NN statistics and per-dispatch kernel durations of the bench workload.
 # usage: bash tools/pass_trace.sh TAG [extra env ...]
 set -u
