@@ -611,6 +611,7 @@ def main():
             "c1": c1_out,
             "c2": c2_out,
             "mean_icp_iterations": float(np.mean(iters)),
+            "library_sources_sha256": source_sha(),
             "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
                                       for k, v in stats.items() if v["launches"]},
             "nn_uncertified_fraction_after_pass0": round(

@@ -52,14 +52,17 @@ struct NNParams {
     int direct_iter;   // ... once its pair has made this many updates
     int kcold, kmax;   // box half-widths (cells): cold start, largest warm box
     int cold_seed;     // seed cold searches with a point of the query's own cell
+    int hmax;          // transform-history slots per pair (max_iteration + 2)
 };
 
 // Correspondence state of one source point, carried from pass to pass (SoA arrays):
 //   corr[i]  nearest target point (sorted index), -1 = none within max_corr
-//   alt[i]   the search's second-nearest point (sorted index), or -1
-//   cert[i]  (q_s, rho): the f32 query point of the search that found corr[i], and a lower
-//            bound rho on the distance from q_s to every target point other than corr[i] and
-//            alt[i] (to every point when corr[i] = -1), metres.
+//   rec[i]   8 bytes: the search's second-nearest point alt (sorted index, or none), the pass s
+//            of the search that left the record, and rho: a lower bound on the distance from
+//            q_s to every target point other than corr[i] and alt (to every point when corr[i]
+//            = -1), metres. q_s, the f32 query point of that search, is not stored: it is
+//            recomputed from the pair's transform at pass s (the transform history), the same
+//            f64 transform of the same source point, so bit for bit the point the search used.
 // Stability certificate: if the query now sits at q with D = |q - q_s|, the nearer w of corr[i]
 // and alt[i] (exact f32 (d2, index) order) is the nearest neighbour whenever |q - w| + D < rho:
 // every other point is at least rho - D away. The pair only swaps places when alt[i] wins. Later
@@ -74,6 +77,17 @@ struct FallbackItem {
     float second_d2;  // second-smallest distance examined (a point other than best)
     float margin;     // rho margin of this query (see prune2)
 };
+
+// rec[i] = (alt | s << 24, rho bits); alt 0xFFFFFF = none (target clouds hold < 2^24 - 1 points,
+// passes < 256: the host checks both, else every pass searches every query)
+constexpr uint32_t REC_NONE = 0xFFFFFFu;
+constexpr int REC_SHIFT = 24;
+__device__ __forceinline__ int2 rec_pack(int alt, int pass, float rho) {
+    return make_int2(int((alt < 0 ? REC_NONE : uint32_t(alt)) | (uint32_t(pass) << REC_SHIFT)),
+                     __float_as_int(rho));
+}
+// transforms of a pair per pass (12 doubles: the top 3 rows), hist[(pair * hmax + pass) * 12]
+constexpr int HIST_STRIDE = 12;
 
 __device__ __forceinline__ bool better(float d2, int idx, float bd2, int bidx) {
     return d2 < bd2 || (d2 == bd2 && idx < bidx);
@@ -693,20 +707,24 @@ __device__ __forceinline__ float motion_margin(const PairState &P, const float4 
 __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &S,
                                            const CloudDev &G, int i, int64_t g,
                                            const NNParams &prm, int32_t *__restrict__ corr,
-                                           int32_t *__restrict__ alt, float4 *__restrict__ cert,
+                                           int2 *__restrict__ rec, const double *hist, int pass,
                                            float &m) {
     const float4 s = lsm_ld(S.xyz, i);
     double x, y, z;
     transform_point(P.T, s, x, y, z);
     const float qx = float(x), qy = float(y), qz = float(z);
-    const float4 c = lsm_ld(cert, g);
-    const double ddx = double(qx) - double(c.x), ddy = double(qy) - double(c.y),
-                 ddz = double(qz) - double(c.z);
+    const int2 rc = lsm_ld(rec, g);
+    const int spass = int(uint32_t(rc.x) >> REC_SHIFT);
+    double xs, ys, zs;   // q_s: the search's query point, from the transform of its pass
+    transform_point(hist + size_t(spass) * HIST_STRIDE, s, xs, ys, zs);
+    const double ddx = double(qx) - double(float(xs)), ddy = double(qy) - double(float(ys)),
+                 ddz = double(qz) - double(float(zs));
     const double delta = sqrt(ddx * ddx + ddy * ddy + ddz * ddz) * (1.0 + 1e-6) + 1e-7;
     const int prev = corr[g];
-    const double r = double(c.w);
+    const double r = double(__int_as_float(rc.y));
     if (prev >= 0) {
-        const int sec = alt[g];
+        const uint32_t araw = uint32_t(rc.x) & REC_NONE;
+        const int sec = araw == REC_NONE ? -1 : int(araw);
         float4 t = lsm_ld(G.xyz, prev);
         float dt = sqd(t, qx, qy, qz);
         bool swap = false;
@@ -726,11 +744,10 @@ __device__ __forceinline__ bool check_query(const PairState &P, const CloudDev &
             if (dt >= prm.maxc2) {
                 // the neighbour left max_corr: no point is within it, none nearer than e
                 corr[g] = -1;
-                alt[g] = -1;
-                cert[g] = make_float4(qx, qy, qz, __double2float_rd(fmin(e * (1.0 - 1e-5), r - delta)));
+                rec[g] = rec_pack(-1, pass, __double2float_rd(fmin(e * (1.0 - 1e-5), r - delta)));
             } else if (swap) {
                 corr[g] = sec;
-                alt[g] = prev;
+                rec[g] = make_int2(int(uint32_t(prev) | (uint32_t(spass) << REC_SHIFT)), rc.y);
             }
             return true;
         }
@@ -781,8 +798,8 @@ __device__ __forceinline__ void flush_stats(const NNStat &ls, unsigned long long
 template <bool CHECK, bool STATS = false>
 __global__ void __launch_bounds__(NN_THREADS) LSM_NN_ATTR
 nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
-          NNParams prm, int32_t *__restrict__ corr, int32_t *__restrict__ alt,
-          float4 *__restrict__ cert, FallbackItem *__restrict__ queue,
+          NNParams prm, int pass, const double *__restrict__ hist, int32_t *__restrict__ corr,
+          int2 *__restrict__ rec, FallbackItem *__restrict__ queue,
           uint32_t *__restrict__ queue_n, uint32_t queue_cap, uint32_t *__restrict__ searched,
           unsigned long long *__restrict__ stats = nullptr) {
     NNStat ls{};
@@ -807,7 +824,9 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         __shared__ float s_m[NN_THREADS];
         __shared__ int32_t s_cnt[NN_THREADS / LSM_WAVE];
         bool need = false;
-        if (live) need = !check_query(P, S, G, i, P.src_off + i, prm, corr, alt, cert, m);
+        if (live)
+            need = !check_query(P, S, G, i, P.src_off + i, prm, corr, rec,
+                                hist + size_t(task.pair) * prm.hmax * HIST_STRIDE, pass, m);
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         const uint64_t bm = __ballot(need);
         if (lane == 0) s_cnt[w] = __popcll(bm);
@@ -863,8 +882,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         push_fallback(pending && lead, task.pair, i, m, t2, queue, queue_n, queue_cap);
         if (lead) {
             corr[g] = pending ? -2 : result;
-            alt[g] = pending ? -1 : a2;
-            if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
+            if (!pending) rec[g] = rec_pack(a2, pass, r);
         }
         if (STATS) {
             if (sub != 0) ls.v[0] = 0;   // one search per query
@@ -887,8 +905,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
     push_fallback(pending, task.pair, i, m, t2, queue, queue_n, queue_cap);
     if (live) {
         corr[g] = pending ? -2 : result;
-        alt[g] = pending ? -1 : a2;
-        if (!pending) cert[g] = make_float4(qp.x, qp.y, qp.z, r);
+        if (!pending) rec[g] = rec_pack(a2, pass, r);
     }
     if (STATS) flush_stats(ls, stats);
 }
@@ -987,7 +1004,7 @@ template <int GL>
 __global__ void __launch_bounds__(LSM_WAVE)
 nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
               const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
-              uint32_t queue_cap, int32_t *__restrict__ corr, float4 *__restrict__ cert,
+              uint32_t queue_cap, int32_t *__restrict__ corr, int2 *__restrict__ rec, int pass,
               unsigned long long *__restrict__ fstats, float far2, int far) {
     // far = 0: the items whose box-search best is within sqrt(far2) (or all when far2 = inf);
     // far = 1: the others (expected to need wider rings: more lanes per query)
@@ -1136,7 +1153,7 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
             const bool hit = t2.bidx >= 0 && t2.bd2 < prm.maxc2;
             fs[5] += hit ? 1 : 0;
             corr[g] = hit ? t2.bidx : -1;
-            cert[g] = make_float4(qx, qy, qz, hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound));
+            rec[g] = rec_pack(-1, pass, hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound));
         }
     }
     if (fstats && sub == 0)
@@ -1364,7 +1381,7 @@ __global__ void __launch_bounds__(LSM_WAVE)
 solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NNParams prm,
              int pass, const double *__restrict__ pair_bytes, uint32_t *__restrict__ active_next,
              double *__restrict__ bytes_next, unsigned long long *__restrict__ src_next,
-             int32_t *__restrict__ flags) {
+             int32_t *__restrict__ flags, double *__restrict__ hist) {
     PairState &P = st[blockIdx.x];
     if (!P.active) return;
     __shared__ double tot[32];
@@ -1433,12 +1450,22 @@ solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NN
         P.Tp[k] = P.T[k];
         P.T[k] = T[k];
     }
+    double *h = hist + (size_t(blockIdx.x) * prm.hmax + pass + 1) * HIST_STRIDE;   // pass + 1's T
+    for (int k = 0; k < HIST_STRIDE; ++k) h[k] = T[k];
     P.iter = pass + 1;
     P.prev_fitness = fitness;
     P.prev_rmse = rmse;
     atomicAdd(active_next, 1u);
     atomicAdd(bytes_next, pair_bytes[blockIdx.x]);
     atomicAdd(src_next, (unsigned long long)P.nsrc);
+}
+
+// slot 0 of every pair's transform history: the initial transform
+__global__ void hist_init_kernel(const PairState *__restrict__ st, int npairs, int hmax,
+                                 double *__restrict__ hist) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= npairs) return;
+    for (int q = 0; q < HIST_STRIDE; ++q) hist[size_t(k) * hmax * HIST_STRIDE + q] = st[k].T[q];
 }
 
 // a pair's final correspondences as a dense array in reference order (for
@@ -1551,8 +1578,13 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     if ((rc = upload(ctx, "i_pbytes", pbytes, &d_pbytes))) return rc;
     const size_t nsrc_tot = size_t(std::max<int64_t>(src_off, 1));
     int32_t *d_corr = (int32_t *)ctx->buf("i_corr", nsrc_tot * 4);
-    float4 *d_cert = (float4 *)ctx->buf("i_cert", nsrc_tot * 16);
-    int32_t *d_alt = (int32_t *)ctx->buf("i_alt", nsrc_tot * 4);
+    int2 *d_rec = (int2 *)ctx->buf("i_rec", nsrc_tot * 8);
+    // every pair's transform at every pass (the certificates' search points): slot 0 is the
+    // initial transform, slot k + 1 the one solve k leaves
+    const int hmax = max_iter + 2;
+    double *d_hist = (double *)ctx->buf("i_hist", size_t(npairs) * hmax * HIST_STRIDE * 8);
+    if (!d_hist) return LSM_ENOMEM;
+    hist_init_kernel<<<int((npairs + 255) / 256), 256, 0, st>>>(d_ps, int(npairs), hmax, d_hist);
     const uint32_t qcap = uint32_t(nsrc_tot);
     FallbackItem *d_q = (FallbackItem *)ctx->buf("i_queue", size_t(qcap) * sizeof(FallbackItem));
     double *d_part = (double *)ctx->buf("i_part", size_t(std::max(slot, 1)) * LSM_ACC * 8);
@@ -1567,7 +1599,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
     int32_t *d_err = (int32_t *)ctx->buf("i_err", 4);
-    if (!d_corr || !d_alt || !d_cert || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
+    if (!d_corr || !d_rec || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
         !d_plan || !d_flags || !d_err || !d_coarse) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
@@ -1581,11 +1613,12 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_srcn, 0, size_t(ncnt) * 8, st));
     if (src_off > 0) {
         LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
-        LSM_HIP_TRY(ctx, hipMemsetAsync(d_alt, 0xff, size_t(src_off) * 4, st));
+        LSM_HIP_TRY(ctx, hipMemsetAsync(d_rec, 0xff, size_t(src_off) * 8, st));
     }
 
     NNParams prm;
     prm.maxc = float(p.max_correspondence_distance);
+    prm.hmax = hmax;
     prm.maxc2 = float(p.max_correspondence_distance * p.max_correspondence_distance);
     prm.method = p.method;
     prm.max_iter = max_iter;
@@ -1650,7 +1683,12 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     // follows the first update, which moves the scans by centimetres to decimetres -- beyond
     // nearly every certificate -- so the check would only add its loads before the search
     const int CERT_FROM = std::max(1, int(lsm_knob("LSM_NN_CERT_FROM", 2)));
-    const bool nocert = lsm_knob("LSM_NN_NOCERT", 0) != 0.0;
+    // (the certificate record holds the search pass in 8 bits and alt in 24: beyond those
+    // bounds every pass searches every query)
+    int64_t max_tgt = 0;
+    for (int64_t k = 0; k < npairs; ++k) max_tgt = std::max<int64_t>(max_tgt, tgt[k]->n);
+    const bool nocert = lsm_knob("LSM_NN_NOCERT", 0) != 0.0 || hmax > 256 ||
+                        max_tgt >= int64_t(REC_NONE);
     double ms0 = 0.0;
     for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
     unsigned long long *d_nst = nullptr;
@@ -1693,17 +1731,17 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             unsigned long long *sp = d_nst + size_t(pass) * NN_NSTAT;
             if (pass < CERT_FROM || nocert)
                 nn_kernel<false, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+                    tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
             else
                 nn_kernel<true, true><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, d_corr, d_alt, d_cert, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
+                    tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
         } else if (pass < CERT_FROM || nocert)
-            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt,
-                                                                d_cert, d_q, d_qn + pass, qcap,
+            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_hist, d_corr,
+                                                                d_rec, d_q, d_qn + pass, qcap,
                                                                 d_sqn + pass);
         else
-            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, d_corr, d_alt,
-                                                               d_cert, d_q, d_qn + pass, qcap,
+            nn_kernel<true><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_hist, d_corr,
+                                                               d_rec, d_q, d_qn + pass, qcap,
                                                                d_sqn + pass);
         ctx->toc("nn", ev);
         ctx->tic("nn_fallback", &ev);
@@ -1711,7 +1749,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             unsigned long long *fst = d_nst ? d_nst + size_t(ncnt) * NN_NSTAT + size_t(pass) * 8
                                             : nullptr;
             nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                            qcap, d_corr, d_cert, fst, INFINITY, 0);
+                                                            qcap, d_corr, d_rec, pass, fst, INFINITY, 0);
         }
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);
@@ -1725,7 +1763,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         ctx->tic("solve", &ev);
         solve_kernel<<<int(npairs), LSM_WAVE, 0, st>>>(d_ps, d_part, prm, pass, d_pbytes,
                                                        d_active + pass, d_bytes + pass,
-                                                       d_srcn + pass, d_flags);
+                                                       d_srcn + pass, d_flags, d_hist);
         ctx->toc("solve", ev);
         plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_coarse, d_plan,
                                                 d_active + pass, d_poll + 3 * pass);
