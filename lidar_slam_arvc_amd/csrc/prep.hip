@@ -596,7 +596,10 @@ __device__ __forceinline__ void cum_add_pt(Cum &c, float4 p, double qx, double q
 
 // Neighbourhoods of at most NSMALL points take Open3D's own covariance arithmetic
 // (normals_small_kernel): normal_from_cum marks them with w = 1 for that pass.
-constexpr int NSMALL = 16;
+#ifndef LSM_NSMALL
+#define LSM_NSMALL 16
+#endif
+constexpr int NSMALL = LSM_NSMALL;
 
 // The normal of covariance A. prior (nullable): EstimateNormals on a cloud that already has
 // normals -- a zero normal keeps the prior one, and the new normal is flipped when it points
@@ -1473,113 +1476,107 @@ void launch_dense_half(hipStream_t st, const Seg *d_segs, int nseg, const CloudD
 // as Open3D does: the ball's members in the search's order (ascending d2, ties by reference
 // index), the nine raw f64 cumulants summed in that order with every product rounded on its
 // own, each divided by n, cov = E[pp^T] - mu mu^T, FastEigen3x3 -- and clears the mark.
-//   stage 1 (normals_small_list_kernel): the marked points of a batch -> one list of (cloud,
-//           point), wave-aggregated appends (a wave's entries stay one run in cell order);
-//   stage 2 (normals_small_kernel): a fixed grid of one-wave workgroups strides over the list,
-//           the member lists in LDS (one slot column per lane).
+//   stage 1 (normals_small_list_kernel): the marked points -> their cloud's list (one append per
+//           workgroup: a workgroup's entries stay one run in cell order);
+//   stage 2 (normals_small_kernel): one lane per list entry over the batch's point segments
+//           (workgroups past their cloud's list return at once; the cloud, and so its point
+//           descriptor, is workgroup-uniform), the member lists in LDS (one slot column per lane).
 __global__ void __launch_bounds__(PT_THREADS)
-normals_small_list_kernel(const Seg *segs, const CloudDev *cd, uint2 *list, uint32_t *cnt) {
+normals_small_list_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, uint32_t *list,
+                          uint32_t *cnt) {
     const Seg s = segs[blockIdx.x];
     const int j = s.start + threadIdx.x;
     const CloudDev &C = cd[s.cloud];
     const bool take = j < C.n && lsm_ld(C.nrm, j).w != 0.f;
-    const uint64_t bm = __ballot(take);
-    if (!bm) return;
-    const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)bm) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(cnt, uint32_t(__popcll(bm)));
-    base = uint32_t(__shfl(int(base), leader, LSM_WAVE));
-    if (take) list[base + __popcll(bm & ((uint64_t(1) << lane) - 1))] = make_uint2(uint32_t(s.cloud), uint32_t(j));
+    if (__syncthreads_or(take))
+        wg_append(take, uint32_t(j), list + geo[s.cloud].pt_off, cnt + s.cloud);
 }
 
-constexpr int SMALL_WG = LSM_WAVE;
-__global__ void __launch_bounds__(SMALL_WG)
-normals_small_kernel(const CloudDev *cd, NormalParams np, const uint2 *list, const uint32_t *cnt) {
-    __shared__ double s_d2[NSMALL * SMALL_WG];
-    __shared__ uint32_t s_ref[NSMALL * SMALL_WG];
-    __shared__ uint32_t s_k[NSMALL * SMALL_WG];
+__global__ void __launch_bounds__(PT_THREADS)
+normals_small_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
+                     const uint32_t *list, const uint32_t *cnt) {
+    __shared__ double s_d2[NSMALL * PT_THREADS];
+    __shared__ uint32_t s_k[NSMALL * PT_THREADS];
+    const Seg s = segs[blockIdx.x];
+    const uint32_t slot = uint32_t(s.start) + threadIdx.x;
+    if (slot >= cnt[s.cloud]) return;
+    const CloudDev C = cd[s.cloud];
+    const int j = int(list[geo[s.cloud].pt_off + slot]);
     double *D = s_d2 + threadIdx.x;
-    uint32_t *Rf = s_ref + threadIdx.x, *Kk = s_k + threadIdx.x;
+    uint32_t *Kk = s_k + threadIdx.x;
     const int cap = np.max_nn < NSMALL ? np.max_nn : NSMALL;
-    const uint32_t total = *cnt;
-    for (uint32_t e = blockIdx.x * SMALL_WG + threadIdx.x; e < total; e += gridDim.x * SMALL_WG) {
-        const uint2 it = list[e];
-        const CloudDev C = cd[it.x];   // per lane: a wave may span two clouds
-        const int j = int(it.y);
-        const float4 qf = lsm_ld(C.xyz, j);
-        const double qx = qf.x, qy = qf.y, qz = qf.z;
-        int m = 0;
-        const GlobalPts pts{C.xyz};
-        ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-            scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
-                Off o;
-                if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
-                const uint32_t ref = lsm_ld(C.perm, k);
-                auto before = [&](int q) {   // (d2, ref) precedes entry q
-                    const double dq = D[q * SMALL_WG];
-                    return o.d2 < dq || (o.d2 == dq && ref < Rf[q * SMALL_WG]);
-                };
-                int pos;
-                if (m < cap) pos = m++;
-                else if (cap > 0 && before(cap - 1)) pos = cap - 1;
-                else return;
-                for (; pos > 0 && before(pos - 1); --pos) {
-                    D[pos * SMALL_WG] = D[(pos - 1) * SMALL_WG];
-                    Rf[pos * SMALL_WG] = Rf[(pos - 1) * SMALL_WG];
-                    Kk[pos * SMALL_WG] = Kk[(pos - 1) * SMALL_WG];
-                }
-                D[pos * SMALL_WG] = o.d2;
-                Rf[pos * SMALL_WG] = ref;
-                Kk[pos * SMALL_WG] = k;
-            });
+    const float4 qf = lsm_ld(C.xyz, j);
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    int m = 0;
+    const NormalsPts pts = normals_pts(C);
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+        scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+            Off o;
+            if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
+            // (d2, reference index) precedes entry q (the reference indices only on exact ties)
+            auto before = [&](int q) {
+                const double dq = D[q * PT_THREADS];
+                return o.d2 < dq ||
+                       (o.d2 == dq && lsm_ld(C.perm, k) < lsm_ld(C.perm, Kk[q * PT_THREADS]));
+            };
+            int pos;
+            if (m < cap) pos = m++;
+            else if (cap > 0 && before(cap - 1)) pos = cap - 1;
+            else return;
+            for (; pos > 0 && before(pos - 1); --pos) {
+                D[pos * PT_THREADS] = D[(pos - 1) * PT_THREADS];
+                Kk[pos * PT_THREADS] = Kk[(pos - 1) * PT_THREADS];
+            }
+            D[pos * PT_THREADS] = o.d2;
+            Kk[pos * PT_THREADS] = k;
         });
-        double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0,
-               c8 = 0.0;
-        for (int q = 0; q < m; ++q) {
-            const float4 p = lsm_ld(C.xyz, Kk[q * SMALL_WG]);
-            const double x = p.x, y = p.y, z = p.z;
-            c0 = lsm_dadd(c0, x);
-            c1 = lsm_dadd(c1, y);
-            c2 = lsm_dadd(c2, z);
-            c3 = lsm_dadd(c3, lsm_dmul(x, x));
-            c4 = lsm_dadd(c4, lsm_dmul(x, y));
-            c5 = lsm_dadd(c5, lsm_dmul(x, z));
-            c6 = lsm_dadd(c6, lsm_dmul(y, y));
-            c7 = lsm_dadd(c7, lsm_dmul(y, z));
-            c8 = lsm_dadd(c8, lsm_dmul(z, z));
-        }
-        sym3 A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
-        if (m >= 3) {
-            const double dn = double(m);
-            c0 = lsm_ddiv(c0, dn);
-            c1 = lsm_ddiv(c1, dn);
-            c2 = lsm_ddiv(c2, dn);
-            c3 = lsm_ddiv(c3, dn);
-            c4 = lsm_ddiv(c4, dn);
-            c5 = lsm_ddiv(c5, dn);
-            c6 = lsm_ddiv(c6, dn);
-            c7 = lsm_ddiv(c7, dn);
-            c8 = lsm_ddiv(c8, dn);
-            A.a00 = lsm_dsub(c3, lsm_dmul(c0, c0));
-            A.a01 = lsm_dsub(c4, lsm_dmul(c0, c1));
-            A.a02 = lsm_dsub(c5, lsm_dmul(c0, c2));
-            A.a11 = lsm_dsub(c6, lsm_dmul(c1, c1));
-            A.a12 = lsm_dsub(c7, lsm_dmul(c1, c2));
-            A.a22 = lsm_dsub(c8, lsm_dmul(c2, c2));
-        }
-        const_cast<float4 *>(C.nrm)[j] =
-            normal_from_cov(A, C.prior_ref ? C.prior_ref + C.perm[j] : nullptr, 0.f);
+    });
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0, c8 = 0.0;
+    for (int q = 0; q < m; ++q) {
+        const float4 p = lsm_ld(C.xyz, Kk[q * PT_THREADS]);
+        const double x = p.x, y = p.y, z = p.z;
+        c0 = lsm_dadd(c0, x);
+        c1 = lsm_dadd(c1, y);
+        c2 = lsm_dadd(c2, z);
+        c3 = lsm_dadd(c3, lsm_dmul(x, x));
+        c4 = lsm_dadd(c4, lsm_dmul(x, y));
+        c5 = lsm_dadd(c5, lsm_dmul(x, z));
+        c6 = lsm_dadd(c6, lsm_dmul(y, y));
+        c7 = lsm_dadd(c7, lsm_dmul(y, z));
+        c8 = lsm_dadd(c8, lsm_dmul(z, z));
     }
+    sym3 A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+    if (m >= 3) {
+        const double dn = double(m);
+        c0 = lsm_ddiv(c0, dn);
+        c1 = lsm_ddiv(c1, dn);
+        c2 = lsm_ddiv(c2, dn);
+        c3 = lsm_ddiv(c3, dn);
+        c4 = lsm_ddiv(c4, dn);
+        c5 = lsm_ddiv(c5, dn);
+        c6 = lsm_ddiv(c6, dn);
+        c7 = lsm_ddiv(c7, dn);
+        c8 = lsm_ddiv(c8, dn);
+        A.a00 = lsm_dsub(c3, lsm_dmul(c0, c0));
+        A.a01 = lsm_dsub(c4, lsm_dmul(c0, c1));
+        A.a02 = lsm_dsub(c5, lsm_dmul(c0, c2));
+        A.a11 = lsm_dsub(c6, lsm_dmul(c1, c1));
+        A.a12 = lsm_dsub(c7, lsm_dmul(c1, c2));
+        A.a22 = lsm_dsub(c8, lsm_dmul(c2, c2));
+    }
+    const_cast<float4 *>(C.nrm)[j] =
+        normal_from_cov(A, C.prior_ref ? C.prior_ref + C.perm[j] : nullptr, 0.f);
 }
 
-// The small-neighbourhood pass over the clouds of `segs` (one lane per point in stage 1).
-// list: scratch of one uint2 per point of the batch; cnt: one scratch word.
+// The small-neighbourhood pass over the clouds of `segs` (K clouds; d_geo: their pt_off into
+// the batch lists). list: scratch of one word per point of the batch; cnt: K scratch words.
 void launch_small_normals(hipStream_t st, const Seg *d_segs, int nseg, const CloudDev *d_cd,
-                          const NormalParams &np, uint2 *list, uint32_t *cnt, int num_cus) {
+                          const GridGeo *d_geo, int K, const NormalParams &np, uint32_t *list,
+                          uint32_t *cnt) {
     if (nseg <= 0) return;
-    (void)hipMemsetAsync(cnt, 0, 4, st);
-    normals_small_list_kernel<<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, list, cnt);
-    normals_small_kernel<<<std::max(1, num_cus * 8), SMALL_WG, 0, st>>>(d_cd, np, list, cnt);
+    (void)hipMemsetAsync(cnt, 0, size_t(K) * 4, st);
+    normals_small_list_kernel<<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, d_geo, list, cnt);
+    normals_small_kernel<<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, d_geo, np, list, cnt);
 }
 
 #ifdef LSM_DIAG
@@ -2048,11 +2045,11 @@ int run_normals(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
     } else {
         normals_kernel<NORMALS_G_DEFAULT><<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_ns);
     }
-    // (the grid's sort keys are dead by now: their buffer holds the small-neighbourhood list)
-    uint2 *slist = (uint2 *)ctx->buf("g_kin", N * 8);
-    uint32_t *scnt = (uint32_t *)ctx->buf("n_small_n", 4);
+    // the small neighbourhoods' lists reuse the dense lists' buffer (dead by now)
+    uint32_t *slist = (uint32_t *)ctx->buf("n_dlist", N * 4);
+    uint32_t *scnt = (uint32_t *)ctx->buf("n_small_n", size_t(K) * 4);
     if (!slist || !scnt) return LSM_ENOMEM;
-    launch_small_normals(st, d_segs, nseg, d_cd, np, slist, scnt, ctx->num_cus);
+    launch_small_normals(st, d_segs, nseg, d_cd, d_geo, K, np, slist, scnt);
     if (d_ns) {
         unsigned long long h[72] = {};
         LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ns, sizeof(h), hipMemcpyDeviceToHost, st));
