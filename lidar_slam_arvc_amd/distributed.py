@@ -48,6 +48,30 @@ def balance_pairs(costs, world: int) -> list:
     return [np.asarray(sorted(v), dtype=np.int64) for v in out]
 
 
+def balance_contiguous(costs, world: int) -> list:
+    """Cost-balanced CONTIGUOUS split of independent pairs over `world` ranks: rank r gets the
+    pair range [cut[r], cut[r + 1]), the cuts chosen so every prefix of ranks carries its share of
+    the total cost as closely as whole pairs allow (cut[r] = the first pair whose cost prefix
+    reaches r / world of the total). Unlike balance_pairs it keeps each rank's pairs adjacent, so
+    re-balancing a contiguous sharding only moves the pairs next to the shard boundaries between
+    neighbouring ranks. Deterministic; returns [a, b) per rank."""
+    c = np.asarray(costs, dtype=np.float64).reshape(-1)
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    n = len(c)
+    pre = np.concatenate([[0.0], np.cumsum(c)])
+    tot = pre[-1]
+    cuts = [0]
+    for r in range(1, world):
+        k = int(np.searchsorted(pre, tot * r / world, side="left"))
+        # the nearer of the two cuts around the target, never behind the previous cut
+        if k > 0 and abs(pre[k - 1] - tot * r / world) <= abs(pre[min(k, n)] - tot * r / world):
+            k -= 1
+        cuts.append(min(max(k, cuts[-1]), n))
+    cuts.append(n)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
 def gather_pair_results(mine: np.ndarray, index: np.ndarray, n_total: int, group=None,
                         device=None) -> np.ndarray:
     """The sequence-level exchange of a sharded batch: every rank contributes

@@ -217,6 +217,27 @@ def _gather_worker(rank, world, port, res, cost, out_q):
     dist.destroy_process_group()
 
 
+
+def test_balance_contiguous():
+    """The contiguous cost-balanced split: ranges tile the pairs in order, are deterministic, and
+    every rank's load is within one pair's cost of the mean (better than the equal-count split on
+    skewed costs)."""
+    rng = np.random.default_rng(3)
+    for n, w in ((4096, 8), (100, 3), (7, 8), (0, 2)):
+        cost = rng.lognormal(0.0, 0.6, n)
+        cost[: n // 5] *= 3.0   # a costly stretch of the sequence
+        parts = distributed.balance_contiguous(cost, w)
+        assert len(parts) == w and parts[0][0] == 0 and parts[-1][1] == n
+        assert all(a <= b for a, b in parts)
+        assert all(parts[r][1] == parts[r + 1][0] for r in range(w - 1))
+        assert parts == distributed.balance_contiguous(cost, w)
+        if n >= 100:
+            load = [cost[a:b].sum() for a, b in parts]
+            assert max(load) - cost.sum() / w <= cost.max() + 1e-9
+            eq = [cost[k * n // w:(k + 1) * n // w].sum() for k in range(w)]
+            assert max(load) <= max(eq)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gather_pair_results_gloo(world):
     """The C4/C5 result exchange (bench.py loop_closure, one all-gather): ranks holding

@@ -37,8 +37,9 @@ def main():
     ps = synthetic.make_revisit_pairs(W * P, seed=args.seed, model=synthetic.HDL64,
                                       processes=16)   # forked workers: before any GPU context
     print(f"{W * P} revisit pairs generated in {time.time() - t0:.1f} s", flush=True)
+    # (pairs and results: the splits below must register every pair exactly once)
     from lidar_slam_arvc_amd import _lib
-    from lidar_slam_arvc_amd.distributed import balance_pairs
+    from lidar_slam_arvc_amd.distributed import balance_contiguous, balance_pairs
     dev = _lib.device(0)
     tg = [dev.upload(s) for s in ps.targets]
     sr = [dev.upload(s) for s in ps.sources]
@@ -63,15 +64,21 @@ def main():
     for idx in contiguous:
         iters[idx] = step(idx)["iterations"]
     nsrc = np.array([dev.info(h)[1] for h in sr], dtype=np.float64)
-    lpt = balance_pairs(nsrc * iters, W)
+    cost = nsrc * iters
+    lpt = balance_pairs(cost, W)
+    bal = [np.arange(a, b) for a, b in balance_contiguous(cost, W)]
     t_c = [timed(idx) for idx in contiguous]
     t_l = [timed(idx) for idx in lpt]
+    t_b = [timed(idx) for idx in bal]
     res = {
         "workload": f"C4 revisit pairs, seed {args.seed}: {W} ranks x {P} pairs, one GPU, ranks "
                     "run one after another (tools/c4_balance.py)",
         "contiguous_ms": [round(t * 1e3, 2) for t in t_c],
         "lpt_ms": [round(t * 1e3, 2) for t in t_l],
         "lpt_pairs_per_rank": [int(len(v)) for v in lpt],
+        "balanced_contiguous_ms": [round(t * 1e3, 2) for t in t_b],
+        "balanced_contiguous_pairs_per_rank": [int(len(v)) for v in bal],
+        "balanced_contiguous_max_over_mean": round(max(t_b) / np.mean(t_b), 4),
         "contiguous_max_over_mean": round(max(t_c) / np.mean(t_c), 4),
         "lpt_max_over_mean": round(max(t_l) / np.mean(t_l), 4),
         "contiguous_max_over_lpt_max": round(max(t_c) / max(t_l), 4),
