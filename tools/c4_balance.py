@@ -37,7 +37,6 @@ def main():
     ps = synthetic.make_revisit_pairs(W * P, seed=args.seed, model=synthetic.HDL64,
                                       processes=16)   # forked workers: before any GPU context
     print(f"{W * P} revisit pairs generated in {time.time() - t0:.1f} s", flush=True)
-    # (pairs and results: the splits below must register every pair exactly once)
     from lidar_slam_arvc_amd import _lib
     from lidar_slam_arvc_amd.distributed import balance_contiguous, balance_pairs
     dev = _lib.device(0)
