@@ -616,8 +616,9 @@ __device__ __forceinline__ float4 normal_from_cov(const sym3 &A, const float4 *p
 }
 
 __device__ __forceinline__ float4 normal_from_cum(const Cum &c, const float4 *prior = nullptr) {
+    // a small neighbourhood only gets the mark: normals_small_kernel computes its normal
+    if (c.n >= 3 && c.n <= NSMALL) return make_float4(0.f, 0.f, 0.f, 1.f);
     sym3 A;
-    const float small = (c.n >= 3 && c.n <= NSMALL) ? 1.f : 0.f;
     if (c.n >= 3) {
         const double inv = 1.0 / double(c.n);
         const double mx = c.sx * inv, my = c.sy * inv, mz = c.sz * inv;
@@ -630,7 +631,7 @@ __device__ __forceinline__ float4 normal_from_cum(const Cum &c, const float4 *pr
     } else {
         A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
     }
-    return normal_from_cov(A, prior, small);
+    return normal_from_cov(A, prior, 0.f);
 }
 
 // Cell range of [q - h, q + h] along one axis, widened by a small margin so every point within
