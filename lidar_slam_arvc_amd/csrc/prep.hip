@@ -600,6 +600,9 @@ __device__ __forceinline__ void cum_add_pt(Cum &c, float4 p, double qx, double q
 #define LSM_NSMALL 16
 #endif
 constexpr int NSMALL = LSM_NSMALL;
+// the sparse half computes neighbourhoods of up to this many points itself (its member lists in
+// LDS: 8 slots keep it at 8 waves per SIMD)
+constexpr int NSMALL_INLINE = NSMALL < 8 ? NSMALL : 8;
 
 // The normal of covariance A. prior (nullable): EstimateNormals on a cloud that already has
 // normals -- a zero normal keeps the prior one, and the new normal is flipped when it points
@@ -1334,6 +1337,78 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
 }
 
+// Open3D's arithmetic for the small neighbourhood of point j, at most CAP points (see
+// normals_small_kernel; C workgroup-uniform): F / Kk the lane's LDS slot columns (stride
+// PT_THREADS, CAP slots).
+template <int CAP>
+__device__ __forceinline__ void small_normal(const CloudDev &C, int j, const NormalParams &np,
+                                             uint32_t *F, uint32_t *Kk) {
+    const int cap = np.max_nn < CAP ? np.max_nn : CAP;
+    const float4 qf = lsm_ld(C.xyz, j);
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    int m = 0;
+    const NormalsPts pts = normals_pts(C);
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+        scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+            Off o;
+            if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
+            const uint32_t fk = __float_as_uint(float(o.d2));   // non-negative: orders as u32
+            auto before = [&](int q) {   // (d2, reference index) precedes entry q
+                const uint32_t fq = F[q * PT_THREADS];
+                if (fk != fq) return fk < fq;
+                const uint32_t kq = Kk[q * PT_THREADS];
+                const double dq = make_off(lsm_ld(C.xyz, kq), qx, qy, qz).d2;
+                return o.d2 < dq || (o.d2 == dq && lsm_ld(C.perm, k) < lsm_ld(C.perm, kq));
+            };
+            int pos;
+            if (m < cap) pos = m++;
+            else if (cap > 0 && before(cap - 1)) pos = cap - 1;
+            else return;
+            for (; pos > 0 && before(pos - 1); --pos) {
+                F[pos * PT_THREADS] = F[(pos - 1) * PT_THREADS];
+                Kk[pos * PT_THREADS] = Kk[(pos - 1) * PT_THREADS];
+            }
+            F[pos * PT_THREADS] = fk;
+            Kk[pos * PT_THREADS] = k;
+        });
+    });
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0, c8 = 0.0;
+    for (int q = 0; q < m; ++q) {
+        const float4 p = lsm_ld(C.xyz, Kk[q * PT_THREADS]);
+        const double x = p.x, y = p.y, z = p.z;
+        c0 = lsm_dadd(c0, x);
+        c1 = lsm_dadd(c1, y);
+        c2 = lsm_dadd(c2, z);
+        c3 = lsm_dadd(c3, lsm_dmul(x, x));
+        c4 = lsm_dadd(c4, lsm_dmul(x, y));
+        c5 = lsm_dadd(c5, lsm_dmul(x, z));
+        c6 = lsm_dadd(c6, lsm_dmul(y, y));
+        c7 = lsm_dadd(c7, lsm_dmul(y, z));
+        c8 = lsm_dadd(c8, lsm_dmul(z, z));
+    }
+    sym3 A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+    if (m >= 3) {
+        const double dn = double(m);
+        c0 = lsm_ddiv(c0, dn);
+        c1 = lsm_ddiv(c1, dn);
+        c2 = lsm_ddiv(c2, dn);
+        c3 = lsm_ddiv(c3, dn);
+        c4 = lsm_ddiv(c4, dn);
+        c5 = lsm_ddiv(c5, dn);
+        c6 = lsm_ddiv(c6, dn);
+        c7 = lsm_ddiv(c7, dn);
+        c8 = lsm_ddiv(c8, dn);
+        A.a00 = lsm_dsub(c3, lsm_dmul(c0, c0));
+        A.a01 = lsm_dsub(c4, lsm_dmul(c0, c1));
+        A.a02 = lsm_dsub(c5, lsm_dmul(c0, c2));
+        A.a11 = lsm_dsub(c6, lsm_dmul(c1, c1));
+        A.a12 = lsm_dsub(c7, lsm_dmul(c1, c2));
+        A.a22 = lsm_dsub(c8, lsm_dmul(c2, c2));
+    }
+    const_cast<float4 *>(C.nrm)[j] =
+        normal_from_cov(A, C.prior_ref ? C.prior_ref + C.perm[j] : nullptr, 0.f);
+}
+
 // Split launch, first half: the points predicted sparse (NL_SPARSE, no LDS). Deferred points are
 // appended to their cloud's dense list dlist[geo.pt_off + ...] (wave-aggregated; the order of
 // the list does not matter: every point's computation is independent of the others).
@@ -1373,18 +1448,25 @@ template <int G>
 __global__ void __launch_bounds__(PT_THREADS) LSM_NSPARSE_ATTR
 normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
                       uint32_t *dlist, uint32_t *dcnt, unsigned long long *stats) {
+    __shared__ uint32_t s_f[NSMALL_INLINE * PT_THREADS];   // small_normal's member lists
+    __shared__ uint32_t s_k[NSMALL_INLINE * PT_THREADS];
     const Seg s = segs[blockIdx.x];
     const CloudDev C = cd[s.cloud];
     const int j = s.start + threadIdx.x;
     const bool valid = j < C.n;
-    bool defer = false;
+    bool defer = false, small = false;
     if (valid) {
         const float4 q = lsm_ld(C.xyz, j);
         CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                    C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
         defer = !hybrid_lane<G, CumAcc, false, NL_SPARSE>(C, j, np, nullptr, nullptr, acc);
         if (stats && !defer) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
+        small = !defer && acc.c.n >= 3 && acc.c.n <= NSMALL_INLINE;
     }
+    // a neighbourhood of at most NSMALL_INLINE points gets Open3D's arithmetic at once, while its
+    // rows are in the cache (the batch's small-neighbourhood pass then takes the larger small
+    // ones, and the few the other paths marked)
+    if (small) small_normal<NSMALL_INLINE>(C, j, np, s_f + threadIdx.x, s_k + threadIdx.x);
     // one append per workgroup: its deferred points stay one run in cell order (the dense
     // half's waves then hold neighbouring points)
     wg_append(defer, uint32_t(j), dlist + geo[s.cloud].pt_off, dcnt + s.cloud);
@@ -1496,77 +1578,14 @@ normals_small_list_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *ge
 __global__ void __launch_bounds__(PT_THREADS)
 normals_small_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
                      const uint32_t *list, const uint32_t *cnt) {
-    __shared__ double s_d2[NSMALL * PT_THREADS];
+    __shared__ uint32_t s_f[NSMALL * PT_THREADS];
     __shared__ uint32_t s_k[NSMALL * PT_THREADS];
     const Seg s = segs[blockIdx.x];
     const uint32_t slot = uint32_t(s.start) + threadIdx.x;
     if (slot >= cnt[s.cloud]) return;
     const CloudDev C = cd[s.cloud];
-    const int j = int(list[geo[s.cloud].pt_off + slot]);
-    double *D = s_d2 + threadIdx.x;
-    uint32_t *Kk = s_k + threadIdx.x;
-    const int cap = np.max_nn < NSMALL ? np.max_nn : NSMALL;
-    const float4 qf = lsm_ld(C.xyz, j);
-    const double qx = qf.x, qy = qf.y, qz = qf.z;
-    int m = 0;
-    const NormalsPts pts = normals_pts(C);
-    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
-            Off o;
-            if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
-            // (d2, reference index) precedes entry q (the reference indices only on exact ties)
-            auto before = [&](int q) {
-                const double dq = D[q * PT_THREADS];
-                return o.d2 < dq ||
-                       (o.d2 == dq && lsm_ld(C.perm, k) < lsm_ld(C.perm, Kk[q * PT_THREADS]));
-            };
-            int pos;
-            if (m < cap) pos = m++;
-            else if (cap > 0 && before(cap - 1)) pos = cap - 1;
-            else return;
-            for (; pos > 0 && before(pos - 1); --pos) {
-                D[pos * PT_THREADS] = D[(pos - 1) * PT_THREADS];
-                Kk[pos * PT_THREADS] = Kk[(pos - 1) * PT_THREADS];
-            }
-            D[pos * PT_THREADS] = o.d2;
-            Kk[pos * PT_THREADS] = k;
-        });
-    });
-    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0, c8 = 0.0;
-    for (int q = 0; q < m; ++q) {
-        const float4 p = lsm_ld(C.xyz, Kk[q * PT_THREADS]);
-        const double x = p.x, y = p.y, z = p.z;
-        c0 = lsm_dadd(c0, x);
-        c1 = lsm_dadd(c1, y);
-        c2 = lsm_dadd(c2, z);
-        c3 = lsm_dadd(c3, lsm_dmul(x, x));
-        c4 = lsm_dadd(c4, lsm_dmul(x, y));
-        c5 = lsm_dadd(c5, lsm_dmul(x, z));
-        c6 = lsm_dadd(c6, lsm_dmul(y, y));
-        c7 = lsm_dadd(c7, lsm_dmul(y, z));
-        c8 = lsm_dadd(c8, lsm_dmul(z, z));
-    }
-    sym3 A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
-    if (m >= 3) {
-        const double dn = double(m);
-        c0 = lsm_ddiv(c0, dn);
-        c1 = lsm_ddiv(c1, dn);
-        c2 = lsm_ddiv(c2, dn);
-        c3 = lsm_ddiv(c3, dn);
-        c4 = lsm_ddiv(c4, dn);
-        c5 = lsm_ddiv(c5, dn);
-        c6 = lsm_ddiv(c6, dn);
-        c7 = lsm_ddiv(c7, dn);
-        c8 = lsm_ddiv(c8, dn);
-        A.a00 = lsm_dsub(c3, lsm_dmul(c0, c0));
-        A.a01 = lsm_dsub(c4, lsm_dmul(c0, c1));
-        A.a02 = lsm_dsub(c5, lsm_dmul(c0, c2));
-        A.a11 = lsm_dsub(c6, lsm_dmul(c1, c1));
-        A.a12 = lsm_dsub(c7, lsm_dmul(c1, c2));
-        A.a22 = lsm_dsub(c8, lsm_dmul(c2, c2));
-    }
-    const_cast<float4 *>(C.nrm)[j] =
-        normal_from_cov(A, C.prior_ref ? C.prior_ref + C.perm[j] : nullptr, 0.f);
+    small_normal<NSMALL>(C, int(list[geo[s.cloud].pt_off + slot]), np, s_f + threadIdx.x,
+                         s_k + threadIdx.x);
 }
 
 // The small-neighbourhood pass over the clouds of `segs` (K clouds; d_geo: their pt_off into
