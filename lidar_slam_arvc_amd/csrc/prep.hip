@@ -596,8 +596,10 @@ __device__ __forceinline__ void cum_add_pt(Cum &c, float4 p, double qx, double q
 
 // Neighbourhoods of at most NSMALL points take Open3D's own covariance arithmetic
 // (normals_small_kernel): normal_from_cum marks them with w = 1 for that pass.
+// (8: headline parity 1999 / 1999 as with 16, the small-neighbourhood pass 2 ms per C3 step
+// instead of 11: DESIGN.md §7)
 #ifndef LSM_NSMALL
-#define LSM_NSMALL 16
+#define LSM_NSMALL 8
 #endif
 constexpr int NSMALL = LSM_NSMALL;
 // the sparse half computes neighbourhoods of up to this many points itself (its member lists in
@@ -703,7 +705,7 @@ constexpr uint32_t SCAN_SLACK = 8;   // scan_run_pred: entry search stops within
 #endif
 constexpr int NORMALS_G_DEFAULT = LSM_NORMALS_G_DEFAULT;
 #ifndef LSM_NORMALS_GD_DEFAULT
-#define LSM_NORMALS_GD_DEFAULT 2
+#define LSM_NORMALS_GD_DEFAULT 4   // dense half, round 4 A/B: 2 / 3 / 4 -> 154.7 / 151.8 / 150.7 ms
 #endif
 constexpr int NORMALS_GD_DEFAULT = LSM_NORMALS_GD_DEFAULT;
 #ifndef LSM_NORMALS_PF
