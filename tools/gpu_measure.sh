@@ -1,7 +1,7 @@
 #!/bin/bash
 # One measurement session on the box: GPU suite + smoke, the default bench line (CPU baseline,
 # C1 and C2 lines) with its rocprof kernel stats, the C4 / C5 lines, the C4 sharding balance.
-# usage: bash tools/gpu_measure.sh TAG [notests]
+# usage: bash tools/gpu_measure.sh TAG [notests|tests] [nobalance]
 set -u
 TAG=${1:-run}
 OUT=gpurun_out/$TAG
@@ -24,5 +24,6 @@ for W in loop_closure ouster_multiscale; do
   find "$OUT/prof_$W" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_$W.csv" \;
   rm -rf "$OUT/prof_$W"
 done
+[ "${3:-}" = "nobalance" ] && exit 0
 timeout -k 10 600 python -u tools/c4_balance.py --out "$OUT/c4_balance.json" > "$OUT/c4_balance.log" 2>&1 || { echo "c4_balance failed"; tail -30 "$OUT/c4_balance.log"; exit 1; }
 tail -12 "$OUT/c4_balance.log"
