@@ -1039,7 +1039,7 @@ constexpr int NL_AUTO = 0, NL_SPARSE = 1, NL_DENSE = 2, NL_DENSE_NR = 4;
 template <int G, typename Acc, bool PH = false, int MODE = NL_AUTO, int PF = LSM_NORMALS_PF>
 __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                             unsigned long long *stats, uint32_t *H, Acc &acc,
-                            NPhase *ph = nullptr) {
+                            NPhase *ph = nullptr, uint32_t *SK = nullptr) {
     const HRow R{H, HSTRIDE == 32 ? (__lane_id() & 31u) : 0u};
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
@@ -1069,6 +1069,8 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
                 if (in && (f < np.r2_lo ||
                            (f <= np.r2_hi && make_off(p, qx, qy, qz).d2 < np.r2))) {
                     acc.add(p, k);
+                    // the first NSMALL_INLINE members (a small neighbourhood: all of them)
+                    if (SK && count < NSMALL_INLINE) SK[count * PT_THREADS] = k;
                     ++count;
                 }
                 return;
@@ -1339,41 +1341,11 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
 }
 
-// Open3D's arithmetic for the small neighbourhood of point j, at most CAP points (see
-// normals_small_kernel; C workgroup-uniform): F / Kk the lane's LDS slot columns (stride
-// PT_THREADS, CAP slots).
-template <int CAP>
-__device__ __forceinline__ void small_normal(const CloudDev &C, int j, const NormalParams &np,
-                                             uint32_t *F, uint32_t *Kk) {
-    const int cap = np.max_nn < CAP ? np.max_nn : CAP;
-    const float4 qf = lsm_ld(C.xyz, j);
-    const double qx = qf.x, qy = qf.y, qz = qf.z;
-    int m = 0;
-    const NormalsPts pts = normals_pts(C);
-    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
-            Off o;
-            if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
-            const uint32_t fk = __float_as_uint(float(o.d2));   // non-negative: orders as u32
-            auto before = [&](int q) {   // (d2, reference index) precedes entry q
-                const uint32_t fq = F[q * PT_THREADS];
-                if (fk != fq) return fk < fq;
-                const uint32_t kq = Kk[q * PT_THREADS];
-                const double dq = make_off(lsm_ld(C.xyz, kq), qx, qy, qz).d2;
-                return o.d2 < dq || (o.d2 == dq && lsm_ld(C.perm, k) < lsm_ld(C.perm, kq));
-            };
-            int pos;
-            if (m < cap) pos = m++;
-            else if (cap > 0 && before(cap - 1)) pos = cap - 1;
-            else return;
-            for (; pos > 0 && before(pos - 1); --pos) {
-                F[pos * PT_THREADS] = F[(pos - 1) * PT_THREADS];
-                Kk[pos * PT_THREADS] = Kk[(pos - 1) * PT_THREADS];
-            }
-            F[pos * PT_THREADS] = fk;
-            Kk[pos * PT_THREADS] = k;
-        });
-    });
+// The normal of point j from its neighbourhood Kk[0 .. m) (LDS column, stride PT_THREADS) in
+// the search's order, in Open3D's arithmetic (ComputeCovariance: raw f64 cumulants in that
+// order, each divided by n; FastEigen3x3).
+__device__ __forceinline__ void small_cov_normal(const CloudDev &C, int j, const uint32_t *Kk,
+                                                 int m) {
     double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0, c8 = 0.0;
     for (int q = 0; q < m; ++q) {
         const float4 p = lsm_ld(C.xyz, Kk[q * PT_THREADS]);
@@ -1409,6 +1381,74 @@ __device__ __forceinline__ void small_normal(const CloudDev &C, int j, const Nor
     }
     const_cast<float4 *>(C.nrm)[j] =
         normal_from_cov(A, C.prior_ref ? C.prior_ref + C.perm[j] : nullptr, 0.f);
+}
+
+// The ordering key of a neighbour: the f32 rounding of its exact d2 (monotone: it orders like d2
+// wherever the keys differ; equal keys fall back to the exact (d2, reference index) order).
+__device__ __forceinline__ bool small_before(const CloudDev &C, double qx, double qy, double qz,
+                                             uint32_t fk, double dk, uint32_t k, uint32_t fq,
+                                             uint32_t kq) {
+    if (fk != fq) return fk < fq;
+    const double dq = make_off(lsm_ld(C.xyz, kq), qx, qy, qz).d2;
+    return dk < dq || (dk == dq && lsm_ld(C.perm, k) < lsm_ld(C.perm, kq));
+}
+
+// Open3D's arithmetic for the small neighbourhood of point j, at most CAP points: the ball walked
+// again, its members kept in the search's order in the lane's LDS columns F / Kk (stride
+// PT_THREADS, CAP slots; C workgroup-uniform). normals_small_kernel.
+template <int CAP>
+__device__ __forceinline__ void small_normal(const CloudDev &C, int j, const NormalParams &np,
+                                             uint32_t *F, uint32_t *Kk) {
+    const int cap = np.max_nn < CAP ? np.max_nn : CAP;
+    const float4 qf = lsm_ld(C.xyz, j);
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    int m = 0;
+    const NormalsPts pts = normals_pts(C);
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+        scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+            Off o;
+            if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
+            const uint32_t fk = __float_as_uint(float(o.d2));   // non-negative: orders as u32
+            auto before = [&](int q) {
+                return small_before(C, qx, qy, qz, fk, o.d2, k, F[q * PT_THREADS],
+                                    Kk[q * PT_THREADS]);
+            };
+            int pos;
+            if (m < cap) pos = m++;
+            else if (cap > 0 && before(cap - 1)) pos = cap - 1;
+            else return;
+            for (; pos > 0 && before(pos - 1); --pos) {
+                F[pos * PT_THREADS] = F[(pos - 1) * PT_THREADS];
+                Kk[pos * PT_THREADS] = Kk[(pos - 1) * PT_THREADS];
+            }
+            F[pos * PT_THREADS] = fk;
+            Kk[pos * PT_THREADS] = k;
+        });
+    });
+    small_cov_normal(C, j, Kk, m);
+}
+
+// The same from the whole neighbourhood already collected in walk order (Kk[0 .. m), the
+// sparse half's scan 1): sorted into the search's order in place, then the normal.
+__device__ __forceinline__ void small_normal_from_list(const CloudDev &C, int j, uint32_t *F,
+                                                       uint32_t *Kk, int m) {
+    const float4 qf = lsm_ld(C.xyz, j);
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    for (int a = 0; a < m; ++a) {
+        const uint32_t k = Kk[a * PT_THREADS];
+        const double dk = make_off(lsm_ld(C.xyz, k), qx, qy, qz).d2;
+        const uint32_t fk = __float_as_uint(float(dk));
+        int pos = a;
+        for (; pos > 0 && small_before(C, qx, qy, qz, fk, dk, k, F[(pos - 1) * PT_THREADS],
+                                       Kk[(pos - 1) * PT_THREADS]);
+             --pos) {
+            F[pos * PT_THREADS] = F[(pos - 1) * PT_THREADS];
+            Kk[pos * PT_THREADS] = Kk[(pos - 1) * PT_THREADS];
+        }
+        F[pos * PT_THREADS] = fk;
+        Kk[pos * PT_THREADS] = k;
+    }
+    small_cov_normal(C, j, Kk, m);
 }
 
 // Split launch, first half: the points predicted sparse (NL_SPARSE, no LDS). Deferred points are
@@ -1457,18 +1497,21 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
     const int j = s.start + threadIdx.x;
     const bool valid = j < C.n;
     bool defer = false, small = false;
+    int small_n = 0;
     if (valid) {
         const float4 q = lsm_ld(C.xyz, j);
         CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                    C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
-        defer = !hybrid_lane<G, CumAcc, false, NL_SPARSE>(C, j, np, nullptr, nullptr, acc);
+        defer = !hybrid_lane<G, CumAcc, false, NL_SPARSE>(C, j, np, nullptr, nullptr, acc,
+                                                           nullptr, s_k + threadIdx.x);
         if (stats && !defer) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
         small = !defer && acc.c.n >= 3 && acc.c.n <= NSMALL_INLINE;
+        small_n = acc.c.n;
     }
-    // a neighbourhood of at most NSMALL_INLINE points gets Open3D's arithmetic at once, while its
-    // rows are in the cache (the batch's small-neighbourhood pass then takes the larger small
-    // ones, and the few the other paths marked)
-    if (small) small_normal<NSMALL_INLINE>(C, j, np, s_f + threadIdx.x, s_k + threadIdx.x);
+    // a neighbourhood of at most NSMALL_INLINE points gets Open3D's arithmetic at once: scan 1
+    // kept its members (the batch's small-neighbourhood pass then takes the larger small ones,
+    // and the few the other paths marked)
+    if (small) small_normal_from_list(C, j, s_f + threadIdx.x, s_k + threadIdx.x, small_n);
     // one append per workgroup: its deferred points stay one run in cell order (the dense
     // half's waves then hold neighbouring points)
     wg_append(defer, uint32_t(j), dlist + geo[s.cloud].pt_off, dcnt + s.cloud);
