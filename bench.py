@@ -511,8 +511,7 @@ def main():
                       for k, v in vj.get("per_kernel_per_step", {}).items()}
         ach = valu / step_s / 1e9 if valu else None
         roof_n = {"bound": "valu", "kernel": "normals_sparse_kernel + normals_dense_kernel + "
-                                             "normals_refine_kernel + normals_small_kernel (the "
-                                             "split launch; " +
+                                             "normals_refine_kernel (the split launch; " +
                                              ("each keyframe's normals when it is first a P2Plane "
                                               "target" if args.normals == "lazy" else
                                               "every keyframe, once per step") +

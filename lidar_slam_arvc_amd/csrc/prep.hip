@@ -594,16 +594,16 @@ __device__ __forceinline__ void cum_add_pt(Cum &c, float4 p, double qx, double q
     c.n += 1;
 }
 
-// Neighbourhoods of at most NSMALL points take Open3D's own covariance arithmetic
-// (normals_small_kernel): normal_from_cum marks them with w = 1 for that pass.
+// Neighbourhoods of at most NSMALL points take Open3D's own covariance arithmetic (small_normal,
+// small_normal_from_list): normal_from_cum only marks them (w = 1) for that step.
 // (8: headline parity 1999 / 1999 as with 16, the small-neighbourhood pass 2 ms per C3 step
 // instead of 11: DESIGN.md §7)
 #ifndef LSM_NSMALL
 #define LSM_NSMALL 8
 #endif
 constexpr int NSMALL = LSM_NSMALL;
-// the sparse half computes neighbourhoods of up to this many points itself (its member lists in
-// LDS: 8 slots keep it at 8 waves per SIMD)
+// the sparse half keeps the first members of each neighbourhood (LDS: 8 slots keep it at 8 waves
+// per SIMD), so it finishes small neighbourhoods of up to this many points without a second walk
 constexpr int NSMALL_INLINE = NSMALL < 8 ? NSMALL : 8;
 
 // The normal of covariance A. prior (nullable): EstimateNormals on a cloud that already has
@@ -621,7 +621,7 @@ __device__ __forceinline__ float4 normal_from_cov(const sym3 &A, const float4 *p
 }
 
 __device__ __forceinline__ float4 normal_from_cum(const Cum &c, const float4 *prior = nullptr) {
-    // a small neighbourhood only gets the mark: normals_small_kernel computes its normal
+    // a small neighbourhood only gets the mark: the kernel's small-normal step computes it
     if (c.n >= 3 && c.n <= NSMALL) return make_float4(0.f, 0.f, 0.f, 1.f);
     sym3 A;
     if (c.n >= 3) {
@@ -1289,6 +1289,139 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
     return true;
 }
 
+// Small neighbourhoods in Open3D's arithmetic (keyframe.py:160-162 -> [O3D]
+// EstimatePerPointCovariances -> ComputeCovariance). A neighbourhood of a few points -- near-
+// collinear points of one distant ring -- has a rank-deficient covariance whose smallest
+// eigenvector the rounding of the cumulants decides, so the centred cumulants of the main path
+// (better numerics, different rounding) would pick a different normal there. A neighbourhood
+// of 3 .. NSMALL points (normal_from_cum leaves only a mark, w = 1) is redone exactly as Open3D
+// does it: the ball's members in the search's order (ascending d2, ties by reference index), the
+// nine raw f64 cumulants summed in that order with every product rounded on its own, each divided
+// by n, cov = E[pp^T] - mu mu^T, FastEigen3x3 (and w = 0). Every kernel that computes normals does
+// this for its own small neighbourhoods right after the main path: the sparse half from the
+// members its scan 1 kept (small_normal_from_list, no second walk), the others by a second walk
+// (small_normal; rare there).
+
+// The normal of point j from its neighbourhood Kk[0 .. m) (LDS, stride STRIDE words) in
+// the search's order, in Open3D's arithmetic (ComputeCovariance: raw f64 cumulants in that
+// order, each divided by n; FastEigen3x3).
+template <int STRIDE>
+__device__ __forceinline__ void small_cov_normal(const CloudDev &C, int j, const uint32_t *Kk,
+                                                 int m) {
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0, c8 = 0.0;
+    for (int q = 0; q < m; ++q) {
+        const float4 p = lsm_ld(C.xyz, Kk[q * STRIDE]);
+        const double x = p.x, y = p.y, z = p.z;
+        c0 = lsm_dadd(c0, x);
+        c1 = lsm_dadd(c1, y);
+        c2 = lsm_dadd(c2, z);
+        c3 = lsm_dadd(c3, lsm_dmul(x, x));
+        c4 = lsm_dadd(c4, lsm_dmul(x, y));
+        c5 = lsm_dadd(c5, lsm_dmul(x, z));
+        c6 = lsm_dadd(c6, lsm_dmul(y, y));
+        c7 = lsm_dadd(c7, lsm_dmul(y, z));
+        c8 = lsm_dadd(c8, lsm_dmul(z, z));
+    }
+    sym3 A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+    if (m >= 3) {
+        const double dn = double(m);
+        c0 = lsm_ddiv(c0, dn);
+        c1 = lsm_ddiv(c1, dn);
+        c2 = lsm_ddiv(c2, dn);
+        c3 = lsm_ddiv(c3, dn);
+        c4 = lsm_ddiv(c4, dn);
+        c5 = lsm_ddiv(c5, dn);
+        c6 = lsm_ddiv(c6, dn);
+        c7 = lsm_ddiv(c7, dn);
+        c8 = lsm_ddiv(c8, dn);
+        A.a00 = lsm_dsub(c3, lsm_dmul(c0, c0));
+        A.a01 = lsm_dsub(c4, lsm_dmul(c0, c1));
+        A.a02 = lsm_dsub(c5, lsm_dmul(c0, c2));
+        A.a11 = lsm_dsub(c6, lsm_dmul(c1, c1));
+        A.a12 = lsm_dsub(c7, lsm_dmul(c1, c2));
+        A.a22 = lsm_dsub(c8, lsm_dmul(c2, c2));
+    }
+    const_cast<float4 *>(C.nrm)[j] =
+        normal_from_cov(A, C.prior_ref ? C.prior_ref + C.perm[j] : nullptr, 0.f);
+}
+
+// The ordering key of a neighbour: the f32 rounding of its exact d2 (monotone: it orders like d2
+// wherever the keys differ; equal keys fall back to the exact (d2, reference index) order).
+__device__ __forceinline__ bool small_before(const CloudDev &C, double qx, double qy, double qz,
+                                             uint32_t fk, double dk, uint32_t k, uint32_t fq,
+                                             uint32_t kq) {
+    if (fk != fq) return fk < fq;
+    const double dq = make_off(lsm_ld(C.xyz, kq), qx, qy, qz).d2;
+    return dk < dq || (dk == dq && lsm_ld(C.perm, k) < lsm_ld(C.perm, kq));
+}
+
+// Open3D's arithmetic for the small neighbourhood of point j, at most CAP points: the ball walked
+// again, its members kept in the search's order in the lane's LDS F / Kk (stride STRIDE words,
+// CAP slots; C workgroup-uniform).
+template <int CAP, int STRIDE>
+__device__ __forceinline__ void small_normal(const CloudDev &C, int j, const NormalParams &np,
+                                             uint32_t *F, uint32_t *Kk) {
+    const int cap = np.max_nn < CAP ? np.max_nn : CAP;
+    const float4 qf = lsm_ld(C.xyz, j);
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    int m = 0;
+    const NormalsPts pts = normals_pts(C);
+    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
+        scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
+            Off o;
+            if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
+            const uint32_t fk = __float_as_uint(float(o.d2));   // non-negative: orders as u32
+            auto before = [&](int q) {
+                return small_before(C, qx, qy, qz, fk, o.d2, k, F[q * STRIDE],
+                                    Kk[q * STRIDE]);
+            };
+            int pos;
+            if (m < cap) pos = m++;
+            else if (cap > 0 && before(cap - 1)) pos = cap - 1;
+            else return;
+            for (; pos > 0 && before(pos - 1); --pos) {
+                F[pos * STRIDE] = F[(pos - 1) * STRIDE];
+                Kk[pos * STRIDE] = Kk[(pos - 1) * STRIDE];
+            }
+            F[pos * STRIDE] = fk;
+            Kk[pos * STRIDE] = k;
+        });
+    });
+    small_cov_normal<STRIDE>(C, j, Kk, m);
+}
+
+// The same from the whole neighbourhood already collected in walk order (Kk[0 .. m), the
+// sparse half's scan 1): sorted into the search's order in place, then the normal.
+template <int STRIDE>
+__device__ __forceinline__ void small_normal_from_list(const CloudDev &C, int j, uint32_t *F,
+                                                       uint32_t *Kk, int m) {
+    const float4 qf = lsm_ld(C.xyz, j);
+    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    for (int a = 0; a < m; ++a) {
+        const uint32_t k = Kk[a * STRIDE];
+        const double dk = make_off(lsm_ld(C.xyz, k), qx, qy, qz).d2;
+        const uint32_t fk = __float_as_uint(float(dk));
+        int pos = a;
+        for (; pos > 0 && small_before(C, qx, qy, qz, fk, dk, k, F[(pos - 1) * STRIDE],
+                                       Kk[(pos - 1) * STRIDE]);
+             --pos) {
+            F[pos * STRIDE] = F[(pos - 1) * STRIDE];
+            Kk[pos * STRIDE] = Kk[(pos - 1) * STRIDE];
+        }
+        F[pos * STRIDE] = fk;
+        Kk[pos * STRIDE] = k;
+    }
+    small_cov_normal<STRIDE>(C, j, Kk, m);
+}
+
+// After a kernel's hybrid_lane: a neighbourhood of 3 .. NSMALL points (normal_from_cum left only
+// a mark) gets Open3D's arithmetic, its member lists in the lane's LDS row (H: HSTRIDE words).
+__device__ __forceinline__ void small_after(const CloudDev &C, int j, const NormalParams &np,
+                                            const CumAcc &acc, uint32_t *H) {
+    static_assert(2 * NSMALL <= HSTRIDE, "small_normal's lists fit a lane's LDS row");
+    if (acc.out && acc.c.n >= 3 && acc.c.n <= NSMALL) small_normal<NSMALL, 1>(C, j, np, H, H + NSMALL);
+}
+
 // Own-cell population from which a point is predicted to have more than max_nn neighbours in
 // its ball (a performance guess only: both outcomes are exact): frac * max_nn * (cell / r)^2,
 // a surface's share of the ball in one cell. On HDL-64 scans with cell = r = 0.3 m and
@@ -1335,121 +1468,13 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
     CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
     hybrid_lane<G>(C, j, np, stats, lds + threadIdx.x * HSTRIDE, acc);
+    small_after(C, j, np, acc, lds + threadIdx.x * HSTRIDE);
     // statistics run only (LSM_NORMALS_STATS): neighbourhood sizes |kNN(max_nn) & ball(r)| -- the
     // algorithmic work of the normals (9 cumulant FMAs per neighbour), summed
     // over 64 counters to spread the atomics
     if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
 }
 
-// The normal of point j from its neighbourhood Kk[0 .. m) (LDS column, stride PT_THREADS) in
-// the search's order, in Open3D's arithmetic (ComputeCovariance: raw f64 cumulants in that
-// order, each divided by n; FastEigen3x3).
-__device__ __forceinline__ void small_cov_normal(const CloudDev &C, int j, const uint32_t *Kk,
-                                                 int m) {
-    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0, c8 = 0.0;
-    for (int q = 0; q < m; ++q) {
-        const float4 p = lsm_ld(C.xyz, Kk[q * PT_THREADS]);
-        const double x = p.x, y = p.y, z = p.z;
-        c0 = lsm_dadd(c0, x);
-        c1 = lsm_dadd(c1, y);
-        c2 = lsm_dadd(c2, z);
-        c3 = lsm_dadd(c3, lsm_dmul(x, x));
-        c4 = lsm_dadd(c4, lsm_dmul(x, y));
-        c5 = lsm_dadd(c5, lsm_dmul(x, z));
-        c6 = lsm_dadd(c6, lsm_dmul(y, y));
-        c7 = lsm_dadd(c7, lsm_dmul(y, z));
-        c8 = lsm_dadd(c8, lsm_dmul(z, z));
-    }
-    sym3 A = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
-    if (m >= 3) {
-        const double dn = double(m);
-        c0 = lsm_ddiv(c0, dn);
-        c1 = lsm_ddiv(c1, dn);
-        c2 = lsm_ddiv(c2, dn);
-        c3 = lsm_ddiv(c3, dn);
-        c4 = lsm_ddiv(c4, dn);
-        c5 = lsm_ddiv(c5, dn);
-        c6 = lsm_ddiv(c6, dn);
-        c7 = lsm_ddiv(c7, dn);
-        c8 = lsm_ddiv(c8, dn);
-        A.a00 = lsm_dsub(c3, lsm_dmul(c0, c0));
-        A.a01 = lsm_dsub(c4, lsm_dmul(c0, c1));
-        A.a02 = lsm_dsub(c5, lsm_dmul(c0, c2));
-        A.a11 = lsm_dsub(c6, lsm_dmul(c1, c1));
-        A.a12 = lsm_dsub(c7, lsm_dmul(c1, c2));
-        A.a22 = lsm_dsub(c8, lsm_dmul(c2, c2));
-    }
-    const_cast<float4 *>(C.nrm)[j] =
-        normal_from_cov(A, C.prior_ref ? C.prior_ref + C.perm[j] : nullptr, 0.f);
-}
-
-// The ordering key of a neighbour: the f32 rounding of its exact d2 (monotone: it orders like d2
-// wherever the keys differ; equal keys fall back to the exact (d2, reference index) order).
-__device__ __forceinline__ bool small_before(const CloudDev &C, double qx, double qy, double qz,
-                                             uint32_t fk, double dk, uint32_t k, uint32_t fq,
-                                             uint32_t kq) {
-    if (fk != fq) return fk < fq;
-    const double dq = make_off(lsm_ld(C.xyz, kq), qx, qy, qz).d2;
-    return dk < dq || (dk == dq && lsm_ld(C.perm, k) < lsm_ld(C.perm, kq));
-}
-
-// Open3D's arithmetic for the small neighbourhood of point j, at most CAP points: the ball walked
-// again, its members kept in the search's order in the lane's LDS columns F / Kk (stride
-// PT_THREADS, CAP slots; C workgroup-uniform). normals_small_kernel.
-template <int CAP>
-__device__ __forceinline__ void small_normal(const CloudDev &C, int j, const NormalParams &np,
-                                             uint32_t *F, uint32_t *Kk) {
-    const int cap = np.max_nn < CAP ? np.max_nn : CAP;
-    const float4 qf = lsm_ld(C.xyz, j);
-    const double qx = qf.x, qy = qf.y, qz = qf.z;
-    int m = 0;
-    const NormalsPts pts = normals_pts(C);
-    ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
-        scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
-            Off o;
-            if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
-            const uint32_t fk = __float_as_uint(float(o.d2));   // non-negative: orders as u32
-            auto before = [&](int q) {
-                return small_before(C, qx, qy, qz, fk, o.d2, k, F[q * PT_THREADS],
-                                    Kk[q * PT_THREADS]);
-            };
-            int pos;
-            if (m < cap) pos = m++;
-            else if (cap > 0 && before(cap - 1)) pos = cap - 1;
-            else return;
-            for (; pos > 0 && before(pos - 1); --pos) {
-                F[pos * PT_THREADS] = F[(pos - 1) * PT_THREADS];
-                Kk[pos * PT_THREADS] = Kk[(pos - 1) * PT_THREADS];
-            }
-            F[pos * PT_THREADS] = fk;
-            Kk[pos * PT_THREADS] = k;
-        });
-    });
-    small_cov_normal(C, j, Kk, m);
-}
-
-// The same from the whole neighbourhood already collected in walk order (Kk[0 .. m), the
-// sparse half's scan 1): sorted into the search's order in place, then the normal.
-__device__ __forceinline__ void small_normal_from_list(const CloudDev &C, int j, uint32_t *F,
-                                                       uint32_t *Kk, int m) {
-    const float4 qf = lsm_ld(C.xyz, j);
-    const double qx = qf.x, qy = qf.y, qz = qf.z;
-    for (int a = 0; a < m; ++a) {
-        const uint32_t k = Kk[a * PT_THREADS];
-        const double dk = make_off(lsm_ld(C.xyz, k), qx, qy, qz).d2;
-        const uint32_t fk = __float_as_uint(float(dk));
-        int pos = a;
-        for (; pos > 0 && small_before(C, qx, qy, qz, fk, dk, k, F[(pos - 1) * PT_THREADS],
-                                       Kk[(pos - 1) * PT_THREADS]);
-             --pos) {
-            F[pos * PT_THREADS] = F[(pos - 1) * PT_THREADS];
-            Kk[pos * PT_THREADS] = Kk[(pos - 1) * PT_THREADS];
-        }
-        F[pos * PT_THREADS] = fk;
-        Kk[pos * PT_THREADS] = k;
-    }
-    small_cov_normal(C, j, Kk, m);
-}
 
 // Split launch, first half: the points predicted sparse (NL_SPARSE, no LDS). Deferred points are
 // appended to their cloud's dense list dlist[geo.pt_off + ...] (wave-aggregated; the order of
@@ -1511,7 +1536,7 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
     // a neighbourhood of at most NSMALL_INLINE points gets Open3D's arithmetic at once: scan 1
     // kept its members (the batch's small-neighbourhood pass then takes the larger small ones,
     // and the few the other paths marked)
-    if (small) small_normal_from_list(C, j, s_f + threadIdx.x, s_k + threadIdx.x, small_n);
+    if (small) small_normal_from_list<PT_THREADS>(C, j, s_f + threadIdx.x, s_k + threadIdx.x, small_n);
     // one append per workgroup: its deferred points stay one run in cell order (the dense
     // half's waves then hold neighbouring points)
     wg_append(defer, uint32_t(j), dlist + geo[s.cloud].pt_off, dcnt + s.cloud);
@@ -1547,6 +1572,7 @@ normals_dense_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, No
     // the rare points that need a refine scan go to the cloud's refine list
     const bool done = hybrid_lane<G, CumAcc, false, NL_DENSE_NR, LSM_NORMALS_PFD>(
         C, j, np, stats, lds + threadIdx.x * HSTRIDE, acc);
+    if (done) small_after(C, j, np, acc, lds + threadIdx.x * HSTRIDE);
     const uint64_t bm = __ballot(!done);
     if (bm) {
         const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)bm) - 1;
@@ -1578,6 +1604,7 @@ normals_refine_kernel(const CloudDev *cd, const GridGeo *geo, NormalParams np,
                    C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
         hybrid_lane<G, CumAcc, false, NL_DENSE, LSM_NORMALS_PFD>(C, j, np, stats,
                                                                  lds + threadIdx.x * HSTRIDE, acc);
+        small_after(C, j, np, acc, lds + threadIdx.x * HSTRIDE);
         if (stats) atomicAdd(stats + 8 + (blockIdx.x & 63), (unsigned long long)acc.c.n);
     }
 }
@@ -1593,55 +1620,6 @@ void launch_dense_half(hipStream_t st, const Seg *d_segs, int nseg, const CloudD
                                                          d_ns, rlist, rcnt);
     normals_refine_kernel<G><<<dim3(K, REFINE_BLOCKS), PT_THREADS, 0, st>>>(d_cd, d_geo, np, rlist,
                                                                            rcnt, d_ns);
-}
-
-// Small neighbourhoods in Open3D's arithmetic (keyframe.py:160-162 -> [O3D]
-// EstimatePerPointCovariances -> ComputeCovariance). A neighbourhood of a few points -- near-
-// collinear points of one distant ring -- has a rank-deficient covariance whose smallest
-// eigenvector the rounding of the cumulants decides, so the centred cumulants of the main path
-// (better numerics, different rounding) would pick a different normal there. For the points
-// normal_from_cum marked (3 <= n <= NSMALL; w = 1) a second pass redoes the neighbourhood exactly
-// as Open3D does: the ball's members in the search's order (ascending d2, ties by reference
-// index), the nine raw f64 cumulants summed in that order with every product rounded on its
-// own, each divided by n, cov = E[pp^T] - mu mu^T, FastEigen3x3 -- and clears the mark.
-//   stage 1 (normals_small_list_kernel): the marked points -> their cloud's list (one append per
-//           workgroup: a workgroup's entries stay one run in cell order);
-//   stage 2 (normals_small_kernel): one lane per list entry over the batch's point segments
-//           (workgroups past their cloud's list return at once; the cloud, and so its point
-//           descriptor, is workgroup-uniform), the member lists in LDS (one slot column per lane).
-__global__ void __launch_bounds__(PT_THREADS)
-normals_small_list_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, uint32_t *list,
-                          uint32_t *cnt) {
-    const Seg s = segs[blockIdx.x];
-    const int j = s.start + threadIdx.x;
-    const CloudDev &C = cd[s.cloud];
-    const bool take = j < C.n && lsm_ld(C.nrm, j).w != 0.f;
-    if (__syncthreads_or(take))
-        wg_append(take, uint32_t(j), list + geo[s.cloud].pt_off, cnt + s.cloud);
-}
-
-__global__ void __launch_bounds__(PT_THREADS)
-normals_small_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, NormalParams np,
-                     const uint32_t *list, const uint32_t *cnt) {
-    __shared__ uint32_t s_f[NSMALL * PT_THREADS];
-    __shared__ uint32_t s_k[NSMALL * PT_THREADS];
-    const Seg s = segs[blockIdx.x];
-    const uint32_t slot = uint32_t(s.start) + threadIdx.x;
-    if (slot >= cnt[s.cloud]) return;
-    const CloudDev C = cd[s.cloud];
-    small_normal<NSMALL>(C, int(list[geo[s.cloud].pt_off + slot]), np, s_f + threadIdx.x,
-                         s_k + threadIdx.x);
-}
-
-// The small-neighbourhood pass over the clouds of `segs` (K clouds; d_geo: their pt_off into
-// the batch lists). list: scratch of one word per point of the batch; cnt: K scratch words.
-void launch_small_normals(hipStream_t st, const Seg *d_segs, int nseg, const CloudDev *d_cd,
-                          const GridGeo *d_geo, int K, const NormalParams &np, uint32_t *list,
-                          uint32_t *cnt) {
-    if (nseg <= 0) return;
-    (void)hipMemsetAsync(cnt, 0, size_t(K) * 4, st);
-    normals_small_list_kernel<<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, d_geo, list, cnt);
-    normals_small_kernel<<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, d_geo, np, list, cnt);
 }
 
 #ifdef LSM_DIAG
@@ -2078,7 +2056,7 @@ int normals_phases(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_
 //     count, finished when the ball holds <= max_nn), the deferred points in full waves of the
 //     clouds' dense lists, and the few the dense half leaves to a refine scan -- or, with
 //     LSM_NORMALS_SPLIT=0 (a test knob: bit-identical), the one-kernel form;
-//   * then the small-neighbourhood pass (Open3D's covariance arithmetic, normals_small_kernel).
+//   * every kernel finishes its small neighbourhoods in Open3D's covariance arithmetic.
 // In statistics mode (lsm_set_timing(ctx, 2)) it also counts the neighbours of every normal
 // (SURVEY.md §8d's algorithmic work) and the points that needed the kNN truncation.
 int run_normals(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
@@ -2110,11 +2088,6 @@ int run_normals(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
     } else {
         normals_kernel<NORMALS_G_DEFAULT><<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_ns);
     }
-    // the small neighbourhoods' lists reuse the dense lists' buffer (dead by now)
-    uint32_t *slist = (uint32_t *)ctx->buf("n_dlist", N * 4);
-    uint32_t *scnt = (uint32_t *)ctx->buf("n_small_n", size_t(K) * 4);
-    if (!slist || !scnt) return LSM_ENOMEM;
-    launch_small_normals(st, d_segs, nseg, d_cd, d_geo, K, np, slist, scnt);
     if (d_ns) {
         unsigned long long h[72] = {};
         LSM_HIP_TRY(ctx, hipMemcpyAsync(h, d_ns, sizeof(h), hipMemcpyDeviceToHost, st));

@@ -3,8 +3,8 @@
 For a few scans (the 8k / 64k parity scans and the target keyframes of chosen headline pairs)
 prints, per neighbourhood-size bucket, how often the GPU's f32 normal equals the C++ oracle's
 (rounded to f32, up to sign) bit for bit, and how often |n . n_ref| > 1 - 1e-6 against the C++
-and the NumPy oracle. Small neighbourhoods (n <= 16) take Open3D's own covariance arithmetic on
-the device (normals_small_kernel), the same arithmetic as the C++ oracle, so they should agree
+and the NumPy oracle. Small neighbourhoods (n <= 8) take Open3D's own covariance arithmetic on
+the device (small_normal / small_normal_from_list), the same arithmetic as the C++ oracle, so they should agree
 bit for bit except where the device's and the host's acos / cos round differently.
 
     python tools/normals_small_check.py [--pairs 333,734,...] [--out FILE.json]

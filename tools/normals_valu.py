@@ -30,8 +30,7 @@ nsteps = (bench["steps"] + bench["warmup"] + 1) if bench else 1
 
 
 def kname(n):
-    m = re.search(r"normals_(sparse_kernel|dense_kernel|refine_kernel|small_list_kernel|"
-                  r"small_kernel|kernel)", n)
+    m = re.search(r"normals_(sparse_kernel|dense_kernel|refine_kernel|kernel)", n)
     return m.group(0) if m else n
 
 
@@ -63,8 +62,8 @@ print(json.dumps({
     "workload": workload,
     "source_sha256": source_sha(),
     "kernel": "every normals launch of a step (split launch: normals_sparse_kernel + "
-              "normals_dense_kernel + normals_refine_kernel, then normals_small_list_kernel + "
-              "normals_small_kernel)",
+              "normals_dense_kernel + normals_refine_kernel, each finishing its small "
+              "neighbourhoods in Open3D's arithmetic)",
     "source": "rocprofv3 --kernel-trace --pmc SQ_* (two passes of 8), bench.py --workload "
               f"{workload} --steps 2 --warmup 1 (tools/pmc_normals_bench.sh)",
     "steps_profiled": nsteps, "normals_mode": mode,
