@@ -20,6 +20,7 @@
 #include <type_traits>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <vector>
 
 #include "fasteigen.h"
@@ -220,27 +221,62 @@ struct VoxGeo {         // per cloud, computed on the host from the f64 bbox
     uint64_t key_off;   // offset of this cloud in the global key space
 };
 
+// ref_coord = (p - voxel_min_bound) / voxel_size ; voxel_index = int(floor(ref_coord)), as a key in
+// the batch's key space
+__device__ __forceinline__ uint64_t voxel_key(float4 p, const VoxGeo &G, double v) {
+    const int64_t kx = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.x, G.ox), v));
+    const int64_t ky = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.y, G.oy), v));
+    const int64_t kz = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.z, G.oz), v));
+    return G.key_off + uint64_t((kx * G.dy + ky) * G.dz + kz);
+}
+
+// Per point: its voxel key, and whether it starts a run -- a maximal stretch of consecutive points
+// (index order) in one voxel. A scan's consecutive points are neighbours on the sensor's rings, so
+// runs are long (Ouster-128 at 0.4 / 0.2 / 0.1 m: 7.3 / 3.6 / 2.2 points on average) and the
+// grouping sorts runs, not points. A cloud's first point starts a run (key spaces are disjoint).
 // KeyT: uint32_t when the batch's key space fits 32 bits (4 radix passes over 4-byte keys)
 template <typename KeyT>
 __global__ void __launch_bounds__(PT_THREADS)
 voxel_keys(const Seg *segs, const float4 *pts, const uint32_t *cloud_off, const uint32_t *cloud_n,
-           const VoxGeo *geo, double v, KeyT *keys, uint32_t *vals) {
+           const VoxGeo *geo, double v, KeyT *keys, uint32_t *run_head) {
+    __shared__ KeyT sk[PT_THREADS];
     const Seg s = segs[blockIdx.x];
-    const int i = s.start + threadIdx.x;
-    if (i >= int(cloud_n[s.cloud])) return;
+    const int t = threadIdx.x, i = s.start + t;
+    const bool valid = i < int(cloud_n[s.cloud]);
     const uint32_t g = cloud_off[s.cloud] + i;
     const VoxGeo G = geo[s.cloud];
-    float4 p = pts[g];
-    // ref_coord = (p - voxel_min_bound) / voxel_size ; voxel_index = int(floor(ref_coord))
-    int64_t kx = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.x, G.ox), v));
-    int64_t ky = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.y, G.oy), v));
-    int64_t kz = (int64_t)(int)floor(lsm_ddiv(lsm_dsub((double)p.z, G.oz), v));
-    keys[g] = KeyT(G.key_off + uint64_t((kx * G.dy + ky) * G.dz + kz));
-    vals[g] = g;
+    KeyT key = 0;
+    if (valid) {
+        key = KeyT(voxel_key(pts[g], G, v));
+        keys[g] = key;
+    }
+    sk[t] = key;
+    __syncthreads();
+    if (!valid) return;
+    bool head;
+    if (i == 0) head = true;
+    else if (t > 0) head = sk[t - 1] != key;
+    else head = KeyT(voxel_key(pts[g - 1], G, v)) != key;
+    run_head[g] = head ? 1u : 0u;
 }
 
-// One thread per sorted entry; voxel heads sum their members in index order (stable sort keeps
-// the original order inside a voxel) exactly like AccumulatedPoint::AddPoint.
+// run heads -> (run key, run start): rid = exclusive scan of the heads; rstart[nruns] = n
+template <typename KeyT>
+__global__ void __launch_bounds__(PT_THREADS)
+voxel_runs(const KeyT *keys, const uint32_t *run_head, const uint32_t *rid, uint32_t n, KeyT *rkeys,
+           uint32_t *rstart) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    if (run_head[g]) {
+        const uint32_t r = rid[g];
+        rkeys[r] = keys[g];
+        rstart[r] = g;
+    }
+    if (g == 0) rstart[rid[n]] = n;
+}
+
+// One thread per sorted run; voxel heads sum their members in index order (the stable sort keeps
+// a voxel's runs in index order) exactly like AccumulatedPoint::AddPoint.
 template <typename KeyT>
 __global__ void __launch_bounds__(PT_THREADS)
 voxel_flags(const KeyT *skeys, uint32_t n, uint32_t *flag) {
@@ -259,53 +295,59 @@ voxel_heads(const uint32_t *flag, const uint32_t *vid_excl, uint32_t n, uint32_t
     if (i == 0) vstart[vid_excl[n]] = n;
 }
 
-// One thread per voxel (the grid covers n threads; those past the voxel count exit): the members
-// summed in index order, as AccumulatedPoint::AddPoint does -- the same left fold in f64 as one
-// thread per head walking its run, with the member loads issued four at a time (the run's length
-// is known from vstart, so the loads need not wait for the run-end test).
+// One thread per voxel (the grid covers the runs; threads past the voxel count exit): the voxel's
+// runs in index order, each run's points in index order -- the left fold in f64 of
+// AccumulatedPoint::AddPoint over the members, with the loads of a long run issued 16 / 4 at a
+// time (a run's length is known from rstart, so the loads need not wait for the run-end test).
 template <typename KeyT>
 __global__ void __launch_bounds__(PT_THREADS)
-voxel_reduce(const KeyT *skeys, const uint32_t *svals, const uint32_t *vid_excl,
-             const uint32_t *vstart, uint32_t n, const float4 *pts, const int32_t *pt_cloud,
+voxel_reduce(const KeyT *skeys, const uint32_t *srun, const uint32_t *rstart, const uint32_t *vid_excl,
+             const uint32_t *vstart, uint32_t nruns, const float4 *pts, const int32_t *pt_cloud,
              const VoxGeo *geo, double *cent, int32_t *vkeys, float4 *vpts, int32_t *vcloud) {
     const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= vid_excl[n]) return;
-    const uint32_t i = vstart[o], e = vstart[o + 1];
+    if (o >= vid_excl[nruns]) return;
+    const uint32_t q0 = vstart[o], q1 = vstart[o + 1];
     double sx = 0.0, sy = 0.0, sz = 0.0;
-    uint32_t j = i;
-    // long runs (voxels of thousands of points near the sensor set the kernel's duration: one
-    // dependent chain each) in batches of 16 loads in flight
-    for (; j + 16 <= e; j += 16) {
-        float4 p[16];
+    uint32_t count = 0, first = 0;
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t r = srun[q];
+        const uint32_t b = rstart[r], e = rstart[r + 1];
+        if (q == q0) first = b;
+        count += e - b;
+        uint32_t j = b;
+        // long runs (voxels of thousands of points near the sensor set the kernel's duration:
+        // one dependent chain each) in batches of 16 loads in flight
+        for (; j + 16 <= e; j += 16) {
+            float4 p[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) p[q] = pts[svals[j + q]];
+            for (int u = 0; u < 16; ++u) p[u] = pts[j + u];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            sx = lsm_dadd(sx, (double)p[q].x);
-            sy = lsm_dadd(sy, (double)p[q].y);
-            sz = lsm_dadd(sz, (double)p[q].z);
+            for (int u = 0; u < 16; ++u) {
+                sx = lsm_dadd(sx, (double)p[u].x);
+                sy = lsm_dadd(sy, (double)p[u].y);
+                sz = lsm_dadd(sz, (double)p[u].z);
+            }
+        }
+        for (; j + 4 <= e; j += 4) {
+            const float4 p0 = pts[j], p1 = pts[j + 1], p2 = pts[j + 2], p3 = pts[j + 3];
+            sx = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sx, (double)p0.x), (double)p1.x), (double)p2.x), (double)p3.x);
+            sy = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sy, (double)p0.y), (double)p1.y), (double)p2.y), (double)p3.y);
+            sz = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sz, (double)p0.z), (double)p1.z), (double)p2.z), (double)p3.z);
+        }
+        for (; j < e; ++j) {
+            const float4 p = pts[j];
+            sx = lsm_dadd(sx, (double)p.x);
+            sy = lsm_dadd(sy, (double)p.y);
+            sz = lsm_dadd(sz, (double)p.z);
         }
     }
-    for (; j + 4 <= e; j += 4) {
-        const uint32_t v0 = svals[j], v1 = svals[j + 1], v2 = svals[j + 2], v3 = svals[j + 3];
-        const float4 p0 = pts[v0], p1 = pts[v1], p2 = pts[v2], p3 = pts[v3];
-        sx = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sx, (double)p0.x), (double)p1.x), (double)p2.x), (double)p3.x);
-        sy = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sy, (double)p0.y), (double)p1.y), (double)p2.y), (double)p3.y);
-        sz = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sz, (double)p0.z), (double)p1.z), (double)p2.z), (double)p3.z);
-    }
-    for (; j < e; ++j) {
-        const float4 p = pts[svals[j]];
-        sx = lsm_dadd(sx, (double)p.x);
-        sy = lsm_dadd(sy, (double)p.y);
-        sz = lsm_dadd(sz, (double)p.z);
-    }
-    const uint64_t key = uint64_t(skeys[i]);
-    const double cnt = double(e - i);
+    const uint64_t key = uint64_t(skeys[q0]);
+    const double cnt = double(count);
     const double cx = lsm_ddiv(sx, cnt), cy = lsm_ddiv(sy, cnt), cz = lsm_ddiv(sz, cnt);
     cent[3 * o] = cx;
     cent[3 * o + 1] = cy;
     cent[3 * o + 2] = cz;
-    const int c = pt_cloud[svals[i]];
+    const int c = pt_cloud[first];
     const VoxGeo G = geo[c];
     const uint64_t local = key - G.key_off;
     const int64_t kz = int64_t(local % uint64_t(G.dz));
@@ -318,10 +360,12 @@ voxel_reduce(const KeyT *skeys, const uint32_t *svals, const uint32_t *vid_excl,
     vcloud[o] = c;
 }
 
-// vb[k] = vid[pstart[k]]: the first voxel id of cloud k (k = K: the voxel total)
-__global__ void vox_cloud_bounds(const uint32_t *vid, const uint32_t *pstart, int n, uint32_t *vb) {
+// vb[k] = vid[rid[pstart[k]]]: the first voxel id of cloud k (k = K: the voxel total); the sort
+// keeps each cloud's runs together (key_off), so cloud k's sorted runs start at its first run id
+__global__ void vox_cloud_bounds(const uint32_t *vid, const uint32_t *rid, const uint32_t *pstart, int n,
+                                 uint32_t *vb) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) vb[k] = vid[pstart[k]];
+    if (k < n) vb[k] = vid[rid[pstart[k]]];
 }
 
 // voxel o's f64 centroid and int32 key into its cloud's arrays (voff: the cloud's first voxel)
@@ -1742,6 +1786,28 @@ inline int bits_for(uint64_t v) {
     return b;
 }
 
+// Radix sorts (grid (cell, x) keys, voxel run keys). rocPRIM's gfx950 defaults sort 8 bits per
+// onesweep pass. 64-bit keys sort 9 bits per pass (the grid's ~63-bit keys: 7 passes, not 8;
+// measured 13.9 -> 13.3 ms of grid per C3 step); 11 bits would need 192 KB of histogram LDS for
+// 64-bit keys, and 11-bit passes over 32-bit keys measured slower than four 8-bit ones.
+// LSM_RADIX_BITS_K32 / LSM_RADIX_BITS_K64 build A/B variants.
+#ifndef LSM_RADIX_BITS_K64
+#define LSM_RADIX_BITS_K64 9
+#endif
+template <int BITS, int BS, int IPT>
+using OnesweepConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 16>, rocprim::kernel_config<BS, IPT>, BITS,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+template <typename Key> struct SortConfigFor { using type = rocprim::default_config; };
+#ifdef LSM_RADIX_BITS_K32
+template <> struct SortConfigFor<uint32_t> { using type = OnesweepConfig<LSM_RADIX_BITS_K32, 512, 16>; };
+#endif
+#ifdef LSM_RADIX_BITS_K64
+template <> struct SortConfigFor<uint64_t> { using type = OnesweepConfig<LSM_RADIX_BITS_K64, 512, 16>; };
+#endif
+template <typename Key> using SortConfig = typename SortConfigFor<Key>::type;
+
 }  // namespace
 
 // ==========================================================================================
@@ -1910,18 +1976,19 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
     const size_t N = std::max<uint32_t>(ntot, 1);
     uint64_t *k_in = (uint64_t *)ctx->buf("v_kin", N * 8);
     uint64_t *k_out = (uint64_t *)ctx->buf("v_kout", N * 8);
-    uint32_t *v_in = (uint32_t *)ctx->buf("v_vin", N * 4);
     uint32_t *v_out = (uint32_t *)ctx->buf("v_vout", N * 4);
     uint32_t *flag = (uint32_t *)ctx->buf("v_flag", N * 4 + 4);
     uint32_t *vid = (uint32_t *)ctx->buf("v_vid", N * 4 + 4);
     uint32_t *vstart = (uint32_t *)ctx->buf("v_vstart", N * 4 + 4);
+    uint32_t *rid = (uint32_t *)ctx->buf("v_rid", N * 4 + 4);
+    uint32_t *rstart = (uint32_t *)ctx->buf("v_rstart", N * 4 + 4);
     int32_t *ptc = (int32_t *)ctx->buf("v_ptc", N * 4);
     double *cent = (double *)ctx->buf("v_cent", N * 24);
     int32_t *vkeys = (int32_t *)ctx->buf("v_keys", N * 12);
     float4 *vpts = (float4 *)ctx->buf("v_pts", N * 16);
     int32_t *vcloud = (int32_t *)ctx->buf("v_vcloud", N * 4);
-    if (!k_in || !k_out || !v_in || !v_out || !flag || !vid || !vstart || !ptc || !cent || !vkeys || !vpts ||
-        !vcloud) {
+    if (!k_in || !k_out || !v_out || !flag || !vid || !vstart || !rid || !rstart || !ptc || !cent ||
+        !vkeys || !vpts || !vcloud) {
         ctx->set_error("scratch allocation failed (voxel)");
         return LSM_ENOMEM;
     }
@@ -1933,43 +2000,59 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
         point_cloud_ids<<<dim3(64, K), 256, 0, st>>>(d_off, d_cnt, K, ptc);
         const int endbit = bits_for(key_off);
         const int nb = int((ntot + PT_THREADS - 1) / PT_THREADS);
-        // keys, stable radix sort, heads, their exclusive scan (voxel ids), per-voxel sums
+        // exclusive scan of n + 1 flags (flag[n] = 0): out[n] = the flag total
+        auto scan_flags = [&](const uint32_t *in, uint32_t *out, uint32_t n) -> int {
+            size_t tb = 0;
+            LSM_HIP_TRY(ctx, rocprim::exclusive_scan(nullptr, tb, in, out, 0u, size_t(n) + 1,
+                                                     rocprim::plus<uint32_t>(), st));
+            void *tp = ctx->buf("scan_tmp", tb);
+            if (!tp) return LSM_ENOMEM;
+            LSM_HIP_TRY(ctx, rocprim::exclusive_scan(tp, tb, in, out, 0u, size_t(n) + 1,
+                                                     rocprim::plus<uint32_t>(), st));
+            return LSM_OK;
+        };
+        // keys and run heads, run ids (scan), run (key, start), stable radix sort of the runs,
+        // voxel heads over the sorted runs and their scan (voxel ids), per-voxel sums
         auto chain = [&](auto *kin, auto *kout) -> int {
             using KeyT = std::remove_pointer_t<decltype(kin)>;
             voxel_keys<KeyT><<<int(segs.size()), PT_THREADS, 0, st>>>(d_segs, *pts, d_off, d_cnt,
-                                                                      d_geo, v, kin, v_in);
+                                                                      d_geo, v, kout, flag);
+            LSM_HIP_TRY(ctx, hipMemsetAsync(flag + ntot, 0, 4, st));
+            int r;
+            if ((r = scan_flags(flag, rid, ntot))) return r;
+            voxel_runs<KeyT><<<nb, PT_THREADS, 0, st>>>(kout, flag, rid, ntot, kin, rstart);
+            uint32_t nruns = 0;   // the sort's length (one read-back)
+            LSM_HIP_TRY(ctx, hipMemcpyAsync(&nruns, rid + ntot, 4, hipMemcpyDeviceToHost, st));
+            LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
+            const rocprim::counting_iterator<uint32_t> run_ids(0u);
             size_t tb = 0;
-            LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(nullptr, tb, kin, kout, v_in, v_out,
-                                                       size_t(ntot), 0, endbit, st));
+            LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<KeyT>>(nullptr, tb, kin, kout, run_ids, v_out,
+                                                                         size_t(nruns), 0, endbit, st));
             void *tp = ctx->buf("sort_tmp", tb);
             if (!tp) return LSM_ENOMEM;
-            LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(tp, tb, kin, kout, v_in, v_out, size_t(ntot),
-                                                       0, endbit, st));
-            voxel_flags<KeyT><<<nb, PT_THREADS, 0, st>>>(kout, ntot, flag);
-            LSM_HIP_TRY(ctx, hipMemsetAsync(flag + ntot, 0, 4, st));
-            tb = 0;
-            LSM_HIP_TRY(ctx, rocprim::exclusive_scan(nullptr, tb, flag, vid, 0u, size_t(ntot) + 1,
-                                                     rocprim::plus<uint32_t>(), st));
-            tp = ctx->buf("scan_tmp", tb);
-            if (!tp) return LSM_ENOMEM;
-            LSM_HIP_TRY(ctx, rocprim::exclusive_scan(tp, tb, flag, vid, 0u, size_t(ntot) + 1,
-                                                     rocprim::plus<uint32_t>(), st));
-            voxel_heads<<<nb, PT_THREADS, 0, st>>>(flag, vid, ntot, vstart);
-            voxel_reduce<KeyT><<<nb, PT_THREADS, 0, st>>>(kout, v_out, vid, vstart, ntot, *pts, ptc,
-                                                          d_geo, cent, vkeys, vpts, vcloud);
+            LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<KeyT>>(tp, tb, kin, kout, run_ids, v_out,
+                                                                         size_t(nruns), 0, endbit, st));
+            const int rb = int((nruns + PT_THREADS - 1) / PT_THREADS);
+            voxel_flags<KeyT><<<rb, PT_THREADS, 0, st>>>(kout, nruns, flag);
+            LSM_HIP_TRY(ctx, hipMemsetAsync(flag + nruns, 0, 4, st));
+            if ((r = scan_flags(flag, vid, nruns))) return r;
+            voxel_heads<<<rb, PT_THREADS, 0, st>>>(flag, vid, nruns, vstart);
+            voxel_reduce<KeyT><<<rb, PT_THREADS, 0, st>>>(kout, v_out, rstart, vid, vstart, nruns, *pts,
+                                                          ptc, d_geo, cent, vkeys, vpts, vcloud);
             return LSM_OK;
         };
         rc = endbit <= 32 ? chain(reinterpret_cast<uint32_t *>(k_in), reinterpret_cast<uint32_t *>(k_out))
                           : chain(k_in, k_out);
         if (rc) return rc;
-        // voxels per cloud: the sort keeps each cloud's keys together (key_off), so cloud k's
-        // voxel ids run from vid[P_k] to vid[P_k+1], P_k = the points of the clouds before it
+        // voxels per cloud: the sort keeps each cloud's runs together (key_off), so cloud k's
+        // voxel ids run from vid[rid[P_k]] to vid[rid[P_k+1]], P_k = the points of the clouds
+        // before it
         std::vector<uint32_t> pstart(size_t(K) + 1, 0);
         for (int k = 0; k < K; ++k) pstart[k + 1] = pstart[k] + cnt[k];
         uint32_t *d_pstart, *d_vb = (uint32_t *)ctx->buf("v_vb", (size_t(K) + 1) * 4);
         if (!d_vb) return LSM_ENOMEM;
         if ((rc = upload_vec(ctx, "v_pstart", pstart, &d_pstart))) return rc;
-        vox_cloud_bounds<<<(K + 1 + 255) / 256, 256, 0, st>>>(vid, d_pstart, K + 1, d_vb);
+        vox_cloud_bounds<<<(K + 1 + 255) / 256, 256, 0, st>>>(vid, rid, d_pstart, K + 1, d_vb);
         // the centroids' boxes for the spatial grid, before the one read-back
         uint32_t *d_voff = (uint32_t *)ctx->buf("v_coff", size_t(K) * 4);
         uint32_t *d_vcnt = (uint32_t *)ctx->buf("v_ccnt", size_t(K) * 4);
@@ -2241,10 +2324,11 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         grid_keys<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, wpts, d_geo, k_in, v_in);
         size_t tmpb = 0;
         const int endbit = 32 + bits_for(cell_total);
-        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(nullptr, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit,
-                                  st));
+        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<uint64_t>>(nullptr, tmpb, k_in, k_out, v_in, v_out,
+                                                                   size_t(ntot), 0, endbit, st));
         void *tmp = ctx->buf("sort_tmp", tmpb);
-        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs(tmp, tmpb, k_in, k_out, v_in, v_out, size_t(ntot), 0, endbit, st));
+        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<uint64_t>>(tmp, tmpb, k_in, k_out, v_in, v_out,
+                                                                   size_t(ntot), 0, endbit, st));
         grid_scatter<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_geo, d_cd, v_out, k_out,
                                                               wpts, d_perm_ptrs, nonempty);
     }
