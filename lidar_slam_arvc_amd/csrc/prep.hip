@@ -295,50 +295,110 @@ voxel_heads(const uint32_t *flag, const uint32_t *vid_excl, uint32_t n, uint32_t
     if (i == 0) vstart[vid_excl[n]] = n;
 }
 
-// One thread per voxel (the grid covers the runs; threads past the voxel count exit): the voxel's
-// runs in index order, each run's points in index order -- the left fold in f64 of
-// AccumulatedPoint::AddPoint over the members, with the loads of a long run issued 16 / 4 at a
-// time (a run's length is known from rstart, so the loads need not wait for the run-end test).
+// Adds pts[b .. e) to the sums in index order (a run of one voxel), its loads BATCH / 4 at a time
+// (the run's length is known, so the loads need not wait for the run-end test).
+template <int BATCH>
+__device__ __forceinline__ void add_run(const float4 *pts, uint32_t b, uint32_t e, double &sx, double &sy,
+                                        double &sz) {
+    uint32_t j = b;
+    for (; j + BATCH <= e; j += BATCH) {
+        float4 p[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) p[u] = pts[j + u];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            sx = lsm_dadd(sx, (double)p[u].x);
+            sy = lsm_dadd(sy, (double)p[u].y);
+            sz = lsm_dadd(sz, (double)p[u].z);
+        }
+    }
+    for (; j + 4 <= e; j += 4) {
+        const float4 p0 = pts[j], p1 = pts[j + 1], p2 = pts[j + 2], p3 = pts[j + 3];
+        sx = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sx, (double)p0.x), (double)p1.x), (double)p2.x), (double)p3.x);
+        sy = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sy, (double)p0.y), (double)p1.y), (double)p2.y), (double)p3.y);
+        sz = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sz, (double)p0.z), (double)p1.z), (double)p2.z), (double)p3.z);
+    }
+    for (; j < e; ++j) {
+        const float4 p = pts[j];
+        sx = lsm_dadd(sx, (double)p.x);
+        sy = lsm_dadd(sy, (double)p.y);
+        sz = lsm_dadd(sz, (double)p.z);
+    }
+}
+
+// run bounds loaded per batch (the next batch's loads are issued before this batch's points are
+// summed, so a voxel of many runs does not wait on its run table run by run)
+#ifndef LSM_VOX_RUN_BATCH
+#define LSM_VOX_RUN_BATCH 8
+#endif
+constexpr uint32_t VOX_RUN_BATCH = LSM_VOX_RUN_BATCH;
+
+// A wave of voxel_reduce takes as long as its voxel of most runs (one dependent chain each), and
+// voxels of many runs are scattered among the small ones (near the sensor: at 0.4 m on an
+// Ouster-128 scan 5 % of the voxels hold half the points, and nearly every wave of 64 consecutive
+// voxels would hold one). voxel_order lists the voxels of more than VOX_RUN_BATCH runs first and
+// the others after them (each class in voxel order: positions from a scan of the wide flags), so
+// the long chains share their waves and the rest finish fast; the results do not depend on the
+// order (each voxel's sums are its own thread's).
+__global__ void __launch_bounds__(PT_THREADS)
+voxel_wide(const uint32_t *vid_excl, const uint32_t *vstart, uint32_t nruns, uint32_t *wide) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nvox = vid_excl[nruns];
+    if (o < nvox) wide[o] = vstart[o + 1] - vstart[o] > VOX_RUN_BATCH ? 1u : 0u;
+    else if (o == nvox) wide[o] = 0u;
+}
+
+__global__ void __launch_bounds__(PT_THREADS)
+voxel_order(const uint32_t *vid_excl, const uint32_t *wide, const uint32_t *wide_excl, uint32_t nruns,
+            uint32_t *order) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nvox = vid_excl[nruns];
+    if (o >= nvox) return;
+    const uint32_t w = wide_excl[o];
+    order[wide[o] ? w : wide_excl[nvox] + (o - w)] = o;
+}
+
+// One thread per voxel, in voxel_order's order (the grid covers the runs; threads past the voxel
+// count exit): the voxel's runs in index order, each run's points in index order -- the left fold
+// in f64 of AccumulatedPoint::AddPoint over the members.
 template <typename KeyT>
 __global__ void __launch_bounds__(PT_THREADS)
 voxel_reduce(const KeyT *skeys, const uint32_t *srun, const uint32_t *rstart, const uint32_t *vid_excl,
-             const uint32_t *vstart, uint32_t nruns, const float4 *pts, const int32_t *pt_cloud,
-             const VoxGeo *geo, double *cent, int32_t *vkeys, float4 *vpts, int32_t *vcloud) {
-    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= vid_excl[nruns]) return;
+             const uint32_t *vstart, const uint32_t *order, uint32_t nruns, const float4 *pts,
+             const int32_t *pt_cloud, const VoxGeo *geo, double *cent, int32_t *vkeys, float4 *vpts,
+             int32_t *vcloud) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= vid_excl[nruns]) return;
+    const uint32_t o = order[t];
     const uint32_t q0 = vstart[o], q1 = vstart[o + 1];
     double sx = 0.0, sy = 0.0, sz = 0.0;
-    uint32_t count = 0, first = 0;
-    for (uint32_t q = q0; q < q1; ++q) {
-        const uint32_t r = srun[q];
-        const uint32_t b = rstart[r], e = rstart[r + 1];
-        if (q == q0) first = b;
-        count += e - b;
-        uint32_t j = b;
-        // long runs (voxels of thousands of points near the sensor set the kernel's duration:
-        // one dependent chain each) in batches of 16 loads in flight
-        for (; j + 16 <= e; j += 16) {
-            float4 p[16];
+    uint32_t count = 0;
+    uint32_t rb[VOX_RUN_BATCH], re[VOX_RUN_BATCH];
+    auto load_batch = [&](uint32_t q) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u) p[u] = pts[j + u];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                sx = lsm_dadd(sx, (double)p[u].x);
-                sy = lsm_dadd(sy, (double)p[u].y);
-                sz = lsm_dadd(sz, (double)p[u].z);
+        for (uint32_t u = 0; u < VOX_RUN_BATCH; ++u) {
+            rb[u] = re[u] = 0;
+            if (q + u < q1) {
+                const uint32_t r = srun[q + u];
+                rb[u] = rstart[r];
+                re[u] = rstart[r + 1];
             }
         }
-        for (; j + 4 <= e; j += 4) {
-            const float4 p0 = pts[j], p1 = pts[j + 1], p2 = pts[j + 2], p3 = pts[j + 3];
-            sx = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sx, (double)p0.x), (double)p1.x), (double)p2.x), (double)p3.x);
-            sy = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sy, (double)p0.y), (double)p1.y), (double)p2.y), (double)p3.y);
-            sz = lsm_dadd(lsm_dadd(lsm_dadd(lsm_dadd(sz, (double)p0.z), (double)p1.z), (double)p2.z), (double)p3.z);
+    };
+    load_batch(q0);
+    const uint32_t first = rb[0];
+    for (uint32_t q = q0; q < q1; q += VOX_RUN_BATCH) {
+        uint32_t cb[VOX_RUN_BATCH], ce[VOX_RUN_BATCH];
+#pragma unroll
+        for (uint32_t u = 0; u < VOX_RUN_BATCH; ++u) {
+            cb[u] = rb[u];
+            ce[u] = re[u];
         }
-        for (; j < e; ++j) {
-            const float4 p = pts[j];
-            sx = lsm_dadd(sx, (double)p.x);
-            sy = lsm_dadd(sy, (double)p.y);
-            sz = lsm_dadd(sz, (double)p.z);
+        if (q + VOX_RUN_BATCH < q1) load_batch(q + VOX_RUN_BATCH);
+#pragma unroll
+        for (uint32_t u = 0; u < VOX_RUN_BATCH; ++u) {
+            count += ce[u] - cb[u];
+            add_run<8>(pts, cb[u], ce[u], sx, sy, sz);
         }
     }
     const uint64_t key = uint64_t(skeys[q0]);
@@ -1746,9 +1806,15 @@ int upload_vec(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out)
         ctx->set_error(std::string("scratch allocation failed: ") + name);
         return LSM_ENOMEM;
     }
-    if (!v.empty())
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice,
-                                        ctx->stream));
+    if (!v.empty()) {   // through the call's pinned staging (see lsm_ctx::stage)
+        void *h = ctx->stage(v.size() * sizeof(T));
+        if (!h) {
+            ctx->set_error("hipHostMalloc failed (upload staging)");
+            return LSM_ENOMEM;
+        }
+        std::memcpy(h, v.data(), v.size() * sizeof(T));
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, h, v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+    }
     *out = d;
     return LSM_OK;
 }
@@ -1982,12 +2048,15 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
     uint32_t *vstart = (uint32_t *)ctx->buf("v_vstart", N * 4 + 4);
     uint32_t *rid = (uint32_t *)ctx->buf("v_rid", N * 4 + 4);
     uint32_t *rstart = (uint32_t *)ctx->buf("v_rstart", N * 4 + 4);
+    uint32_t *vorder = (uint32_t *)ctx->buf("v_order", N * 4);
+    uint32_t *vwex = (uint32_t *)ctx->buf("v_wex", N * 4 + 4);
     int32_t *ptc = (int32_t *)ctx->buf("v_ptc", N * 4);
     double *cent = (double *)ctx->buf("v_cent", N * 24);
     int32_t *vkeys = (int32_t *)ctx->buf("v_keys", N * 12);
     float4 *vpts = (float4 *)ctx->buf("v_pts", N * 16);
     int32_t *vcloud = (int32_t *)ctx->buf("v_vcloud", N * 4);
-    if (!k_in || !k_out || !v_out || !flag || !vid || !vstart || !rid || !rstart || !ptc || !cent ||
+    if (!k_in || !k_out || !v_out || !flag || !vid || !vstart || !rid || !rstart || !vorder || !vwex || !ptc ||
+        !cent ||
         !vkeys || !vpts || !vcloud) {
         ctx->set_error("scratch allocation failed (voxel)");
         return LSM_ENOMEM;
@@ -2037,8 +2106,13 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
             LSM_HIP_TRY(ctx, hipMemsetAsync(flag + nruns, 0, 4, st));
             if ((r = scan_flags(flag, vid, nruns))) return r;
             voxel_heads<<<rb, PT_THREADS, 0, st>>>(flag, vid, nruns, vstart);
-            voxel_reduce<KeyT><<<rb, PT_THREADS, 0, st>>>(kout, v_out, rstart, vid, vstart, nruns, *pts,
-                                                          ptc, d_geo, cent, vkeys, vpts, vcloud);
+            // voxels <= runs: the flags and their scan cover nruns + 1 entries (past nvox: 0)
+            voxel_wide<<<int((nruns + 1 + PT_THREADS - 1) / PT_THREADS), PT_THREADS, 0, st>>>(vid, vstart, nruns,
+                                                                                               flag);
+            if ((r = scan_flags(flag, vwex, nruns))) return r;
+            voxel_order<<<rb, PT_THREADS, 0, st>>>(vid, flag, vwex, nruns, vorder);
+            voxel_reduce<KeyT><<<rb, PT_THREADS, 0, st>>>(kout, v_out, rstart, vid, vstart, vorder, nruns,
+                                                          *pts, ptc, d_geo, cent, vkeys, vpts, vcloud);
             return LSM_OK;
         };
         rc = endbit <= 32 ? chain(reinterpret_cast<uint32_t *>(k_in), reinterpret_cast<uint32_t *>(k_out))
@@ -2186,6 +2260,7 @@ int run_normals(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
 
 int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params &p,
                    int64_t *n_out) {
+    ctx->stage_reset();   // the previous call's staged uploads have landed
     hipStream_t st = ctx->stream;
     const int K = int(clouds.size());
     int rc;
@@ -2373,6 +2448,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
 }
 
 int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
+    ctx->stage_reset();   // the previous call's staged uploads have landed
     hipStream_t st = ctx->stream;
     int rc;
     // one pass per (radius, max_nn) of the pending clouds
@@ -2630,6 +2706,7 @@ mutual_kernel(const int32_t *__restrict__ ij, int na, const int32_t *__restrict_
 }  // namespace
 
 int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn) {
+    ctx->stage_reset();   // the previous call's staged uploads have landed
     hipStream_t st = ctx->stream;
     const int n = int(c->n);
     if (!c->d_fpfh || c->fpfh_cap < n) {

@@ -23,10 +23,14 @@ elif len(sys.argv) > 2:
 
 
 def short(n):
-    n = n.split("(")[0]
-    for k in ("radix_sort", "scan_impl", "lookback", "fillBuffer", "copyBuffer"):
+    for k in ("radix_sort", "scan_impl", "lookback", "fillBuffer", "copyBuffer", "onesweep"):
         if k in n:
             return k
+    if n.startswith("void "):
+        n = n[5:]
+    n = n.replace("(anonymous namespace)::", "")
+    for c in "(<":
+        n = n.split(c)[0]
     return n.split("::")[-1][:40]
 
 
