@@ -115,6 +115,8 @@ def parse():
                     help="skip the lines of configs C1 (8k-point P2P pairs) and C2 (one 64k "
                          "P2Plane pair), CPU and GPU")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
+    ap.add_argument("--grid-cell-scales", default="",
+                    help="ouster_multiscale: comma-separated grid cell per voxel scale (overrides --grid-cell)")
     ap.add_argument("--seq-cache", default="",
                     help="profiling / A/B runs: load the synthetic data from this .npz if it "
                          "holds this workload's, else generate it and save it there")
@@ -381,11 +383,13 @@ def main():
     if ouster:
         from lidar_slam_arvc_amd.multiscale import MultiScaleSet
         ms = MultiScaleSet(dev, ids)                 # per-scale device clones, made once
+        grid_cells = ([float(c) for c in args.grid_cell_scales.split(",")]
+                      if args.grid_cell_scales else None)
 
         n_fine = []   # points per scan at the finest scale: the same every step, read once
 
         def step():
-            ms.preprocess(want_normals=wn_mode, grid_cell=args.grid_cell)
+            ms.preprocess(want_normals=wn_mode, grid_cell=args.grid_cell, grid_cells=grid_cells)
             stages = ms.register(list(range(1, P + 1)), list(range(P)), seq.priors,
                                  method=args.method, arrays=True)
             res = stages[-1]

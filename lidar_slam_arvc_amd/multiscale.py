@@ -39,11 +39,20 @@ class MultiScaleSet:
             self.release()
             raise
 
-    def preprocess(self, want_normals=True, **prep_kwargs):
-        """KeyFrame.pre_process at every scale: filter -> voxel_down_sample(v) -> normals."""
-        for v, hs in zip(self.scales, self.handles):
-            self.dev.preprocess(hs, _lib.prep_params(voxel_size=v, want_normals=want_normals,
-                                                     **prep_kwargs))
+    def preprocess(self, want_normals=True, grid_cells=None, **prep_kwargs):
+        """KeyFrame.pre_process at every scale: filter -> voxel_down_sample(v) -> normals.
+        grid_cells: the spatial grid's cell per scale (None: ``grid_cell`` of prep_kwargs, or the
+        library's choice); the grid only indexes the points, results do not depend on it."""
+        if grid_cells is not None:
+            grid_cells = tuple(float(c) for c in grid_cells)
+            if len(grid_cells) != len(self.scales):
+                raise ValueError("one grid cell per scale")
+            prep_kwargs.pop("grid_cell", None)
+        for k, (v, hs) in enumerate(zip(self.scales, self.handles)):
+            kw = dict(prep_kwargs)
+            if grid_cells is not None:
+                kw["grid_cell"] = grid_cells[k]
+            self.dev.preprocess(hs, _lib.prep_params(voxel_size=v, want_normals=want_normals, **kw))
 
     def register(self, src_idx, tgt_idx, inits=None, max_corr=DEFAULT_MAX_CORR,
                  method="p2plane", max_iteration=30, arrays=False):

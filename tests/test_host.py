@@ -238,6 +238,43 @@ def test_balance_contiguous():
             assert max(load) <= max(eq)
 
 
+def test_multiscale_set_prep_params_per_scale():
+    """MultiScaleSet's host logic without a device: one clone per scale and raw scan, each scale
+    pre-processed with its voxel size, and the per-scale grid cells (or the shared one) passed on."""
+    from lidar_slam_arvc_amd.multiscale import MultiScaleSet
+
+    class Dev:
+        def __init__(self):
+            self.n, self.calls, self.released = 100, [], []
+
+        def clone(self, h):
+            self.n += 1
+            return self.n
+
+        def preprocess(self, hs, prm):
+            self.calls.append((list(hs), prm.voxel_size, prm.grid_cell))
+
+        def release(self, h):
+            self.released.append(h)
+
+    d = Dev()
+    ms = MultiScaleSet(d, [1, 2], scales=(0.4, 0.2, 0.1))
+    assert [len(h) for h in ms.handles] == [2, 2, 2]
+    ms.preprocess(want_normals=False, grid_cells=(1.0, 0.5, 0.375))
+    assert [(v, g) for _, v, g in d.calls] == [(0.4, 1.0), (0.2, 0.5), (0.1, 0.375)]
+    assert [hs for hs, _, _ in d.calls] == ms.handles
+    d.calls.clear()
+    ms.preprocess(want_normals=False, grid_cell=0.6)
+    assert [g for _, _, g in d.calls] == [0.6, 0.6, 0.6]
+    d.calls.clear()
+    ms.preprocess(want_normals=False, grid_cell=0.6, grid_cells=(0.7, 0.7, 0.7))
+    assert [g for _, _, g in d.calls] == [0.7, 0.7, 0.7]
+    with pytest.raises(ValueError):
+        ms.preprocess(grid_cells=(1.0, 0.5))
+    ms.release()
+    assert sorted(d.released) == list(range(101, 107))
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gather_pair_results_gloo(world):
     """The C4/C5 result exchange (bench.py loop_closure, one all-gather): ranks holding
