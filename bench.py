@@ -20,6 +20,7 @@ P2P pairs) and C2 (one 64k P2Plane pair): the CPU implementation, and the same p
 from __future__ import annotations
 
 import argparse
+import functools
 import json
 import os
 import threading
@@ -55,9 +56,36 @@ def source_sha() -> str:
     return h.hexdigest()
 
 
+# The kernels whose machine code a PMC count depends on: the counted kernels and the grid build
+# that lays out what they read (the clouds themselves are pinned bit-exact by the parity tests).
+PMC_KERNELS = {
+    "nn_traffic.json": ("nn_kernel", "grid_keys", "grid_scatter", "grid_fill", "block_mask_kernel"),
+    "normals_valu.json": ("normals_sparse_kernel", "normals_dense_kernel", "normals_refine_kernel",
+                          "grid_keys", "grid_scatter", "grid_fill", "block_mask_kernel"),
+}
+
+
+@functools.lru_cache(maxsize=None)
+def kernel_sha(prefixes) -> dict:
+    """Hashes of the loaded library's gfx950 machine code of the kernels named by `prefixes`
+    (tools/kernel_hash.py: disassembly with addresses made relative); {} when unavailable."""
+    try:
+        import importlib.util
+        from lidar_slam_arvc_amd import _lib
+        spec = importlib.util.spec_from_file_location("kernel_hash",
+                                                      os.path.join(ROOT, "tools", "kernel_hash.py"))
+        kh = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(kh)
+        return kh.kernel_hashes(_lib.LIB_PATH, prefixes)
+    except Exception:
+        return {}
+
+
 def pmc_entry(name: str, workload: str, pairs: int, mode: str | None = None):
     """The committed PMC summary of this workload (profiles/<name>, keyed by workload), or
-    (None, reason) when it is absent, of another size or mode, or counted on other sources."""
+    (None, reason) when it is absent, of another size or mode, or counted on other code. A count
+    holds for the library sources it was counted on (source_sha256) and for any build whose
+    counted kernels and grid build compile to the same machine code (kernel_sha)."""
     path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None, "no PMC file"
@@ -67,9 +95,11 @@ def pmc_entry(name: str, workload: str, pairs: int, mode: str | None = None):
         return None, f"no PMC count for {workload}"
     if e.get("pairs_per_gpu") != pairs or (mode is not None and e.get("normals_mode") != mode):
         return None, "PMC count of another configuration"
-    if e.get("source_sha256") != source_sha():
-        return None, "stale: PMC counted on other library sources"
-    return e, None
+    if e.get("source_sha256") == source_sha():
+        return e, None
+    if e.get("kernel_sha") and e["kernel_sha"] == kernel_sha(tuple(PMC_KERNELS[name])):
+        return e, None
+    return None, "stale: PMC counted on other kernel code"
 
 
 def parse():

@@ -12,7 +12,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import source_sha  # noqa: E402
+from bench import PMC_KERNELS, kernel_sha, source_sha  # noqa: E402
 
 out = sys.argv[1]
 workload = sys.argv[2] if len(sys.argv) > 2 else "hdl64_seq"
@@ -44,6 +44,7 @@ hbm = (2.0 * fetch_kb + write_kb) * 1024.0 / max(passes, 1)
 print(json.dumps({
     "workload": workload,
     "source_sha256": source_sha(),
+    "kernel_sha": kernel_sha(tuple(PMC_KERNELS["nn_traffic.json"])),
     "kernel": "correspondence pass (nn_kernel + nn_fallback)",
     "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
               f"bench.py --workload {workload} --steps 2 --warmup 1 (tools/pmc_nn.sh)",

@@ -16,7 +16,7 @@ import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import source_sha  # noqa: E402
+from bench import PMC_KERNELS, kernel_sha, source_sha  # noqa: E402
 
 out = sys.argv[1]
 workload = sys.argv[2] if len(sys.argv) > 2 else "hdl64_seq"
@@ -61,6 +61,7 @@ mode = bench["config"]["normals"].split(", ")[-1] if bench else None
 print(json.dumps({
     "workload": workload,
     "source_sha256": source_sha(),
+    "kernel_sha": kernel_sha(tuple(PMC_KERNELS["normals_valu.json"])),
     "kernel": "every normals launch of a step (split launch: normals_sparse_kernel + "
               "normals_dense_kernel + normals_refine_kernel, each finishing its small "
               "neighbourhoods in Open3D's arithmetic)",
