@@ -65,10 +65,16 @@ PMC_KERNELS = {
 }
 
 
+_GPU_STARTED = [False]   # set before the first GPU call: no child processes from then on
+
+
 @functools.lru_cache(maxsize=None)
 def kernel_sha(prefixes) -> dict:
     """Hashes of the loaded library's gfx950 machine code of the kernels named by `prefixes`
-    (tools/kernel_hash.py: disassembly with addresses made relative); {} when unavailable."""
+    (tools/kernel_hash.py: disassembly with addresses made relative); {} when unavailable, or
+    when first asked for after the GPU was initialised (bench.main computes them before)."""
+    if _GPU_STARTED[0]:
+        return {}
     try:
         import importlib.util
         from lidar_slam_arvc_amd import _lib
@@ -382,6 +388,11 @@ def main():
         # C2: one 64k HDL-64 pair, seed 2
         c2 = synthetic.make_sequence(2, seed=2, model=synthetic.HDL64, processes=procs)
     cpu_threads = args.cpu_threads or usable_cores()
+    # the kernel hashes spawn llvm-objdump: before this process touches the GPU (every rank: the
+    # normals' PMC lookup runs on all of them)
+    for kernels in PMC_KERNELS.values():
+        kernel_sha(tuple(kernels))
+    _GPU_STARTED[0] = True
 
     import torch
     import torch.distributed as dist
