@@ -76,36 +76,6 @@ void *lsm_ctx::host_pinned_extra(size_t bytes) {
     return pinned2;
 }
 
-void *lsm_ctx::stage(size_t bytes) {
-    bytes = (bytes + 255) & ~size_t(255);
-    if (stage_chunks.empty() || stage_used + bytes > stage_chunks.back().second) {
-        size_t cap = stage_chunks.empty() ? size_t(1) << 20 : stage_chunks.back().second * 2;
-        cap = std::max(cap, bytes);
-        void *p = nullptr;
-        if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
-        stage_chunks.push_back({p, cap});
-        stage_used = 0;
-    }
-    void *r = static_cast<char *>(stage_chunks.back().first) + stage_used;
-    stage_used += bytes;
-    return r;
-}
-
-void lsm_ctx::stage_reset() {
-    if (stream) (void)hipStreamSynchronize(stream);
-    if (stage_chunks.size() > 1) {   // one chunk of the total size from now on
-        size_t total = 0;
-        for (auto &c : stage_chunks) {
-            total += c.second;
-            (void)hipHostFree(c.first);
-        }
-        stage_chunks.clear();
-        void *p = nullptr;
-        if (hipHostMalloc(&p, total, hipHostMallocDefault) == hipSuccess) stage_chunks.push_back({p, total});
-    }
-    stage_used = 0;
-}
-
 hipEvent_t lsm_ctx::get_event() {
     if (!event_pool.empty()) {
         hipEvent_t e = event_pool.back();
@@ -236,7 +206,6 @@ int lsm_free(lsm_ctx *ctx) {
     }
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->pinned2) (void)hipHostFree(ctx->pinned2);
-    for (auto &c : ctx->stage_chunks) (void)hipHostFree(c.first);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return LSM_OK;

@@ -1485,15 +1485,9 @@ int upload(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out) {
         ctx->set_error(std::string("scratch allocation failed: ") + name);
         return LSM_ENOMEM;
     }
-    if (!v.empty()) {   // through the call's pinned staging (see lsm_ctx::stage)
-        void *h = ctx->stage(v.size() * sizeof(T));
-        if (!h) {
-            ctx->set_error("hipHostMalloc failed (upload staging)");
-            return LSM_ENOMEM;
-        }
-        std::memcpy(h, v.data(), v.size() * sizeof(T));
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, h, v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
-    }
+    if (!v.empty())
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice,
+                                        ctx->stream));
     *out = d;
     return LSM_OK;
 }
@@ -1502,7 +1496,6 @@ int upload(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out) {
 
 int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const double *init,
                 const lsm_icp_params &p, lsm_icp_result *out) {
-    ctx->stage_reset();   // the previous call's staged uploads have landed
     hipStream_t st = ctx->stream;
     int rc;
     // unique clouds -> CloudDev table

@@ -87,15 +87,6 @@ struct lsm_ctx {
     void *host_pinned(size_t bytes);
     void *host_pinned_extra(size_t bytes);   // a second, fixed 4 KiB pinned area
     void *pinned2 = nullptr;
-    // Pinned staging for a call's host -> device uploads (per-cloud tables, launch segments): a
-    // copy from pageable memory makes the host wait for the stream to drain, idling the GPU while
-    // the host then refills the queue; copies from pinned memory are queued like launches.
-    // stage() hands out space that stays valid until stage_reset(), which synchronises the stream
-    // first and is called at the entry of the batch calls.
-    std::vector<std::pair<void *, size_t>> stage_chunks;
-    size_t stage_used = 0;
-    void *stage(size_t bytes);
-    void stage_reset();
     hipEvent_t get_event();
     // bracket a launch with events when timing is on
     void tic(const char *name, hipEvent_t *a);

@@ -1889,15 +1889,9 @@ int upload_vec(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out)
         ctx->set_error(std::string("scratch allocation failed: ") + name);
         return LSM_ENOMEM;
     }
-    if (!v.empty()) {   // through the call's pinned staging (see lsm_ctx::stage)
-        void *h = ctx->stage(v.size() * sizeof(T));
-        if (!h) {
-            ctx->set_error("hipHostMalloc failed (upload staging)");
-            return LSM_ENOMEM;
-        }
-        std::memcpy(h, v.data(), v.size() * sizeof(T));
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, h, v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
-    }
+    if (!v.empty())
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice,
+                                        ctx->stream));
     *out = d;
     return LSM_OK;
 }
@@ -2343,7 +2337,6 @@ int run_normals(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
 
 int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params &p,
                    int64_t *n_out) {
-    ctx->stage_reset();   // the previous call's staged uploads have landed
     hipStream_t st = ctx->stream;
     const int K = int(clouds.size());
     int rc;
@@ -2531,7 +2524,6 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
 }
 
 int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
-    ctx->stage_reset();   // the previous call's staged uploads have landed
     hipStream_t st = ctx->stream;
     int rc;
     // one pass per (radius, max_nn) of the pending clouds
@@ -2789,7 +2781,6 @@ mutual_kernel(const int32_t *__restrict__ ij, int na, const int32_t *__restrict_
 }  // namespace
 
 int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn) {
-    ctx->stage_reset();   // the previous call's staged uploads have landed
     hipStream_t st = ctx->stream;
     const int n = int(c->n);
     if (!c->d_fpfh || c->fpfh_cap < n) {
