@@ -1,6 +1,7 @@
 """CPU: the C-ABI library (load + exported symbols, no compute), host logic, data formats, and
 the multi-rank pose composition over gloo."""
 import ctypes as C
+import json
 import os
 import re
 
@@ -25,6 +26,22 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     assert sorted(_lib.EXPORTED) == syms
+
+
+def test_pmc_counts_match_the_built_kernels():
+    """The committed PMC counts (profiles/nn_traffic.json, normals_valu.json) apply to the in-tree
+    build: every workload's entry carries the source hash or the machine-code hashes
+    (tools/kernel_hash.py) of the kernels it counted, and those match the built library -- so the
+    bench line's traffic and VALU figures describe the code that runs."""
+    import bench
+    for name in ("nn_traffic.json", "normals_valu.json"):
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            entries = json.load(f)
+        ks = bench.kernel_sha(tuple(bench.PMC_KERNELS[name]))
+        assert ks and all(any(k.startswith(p) for k in ks) for p in bench.PMC_KERNELS[name])
+        for workload, e in entries.items():
+            assert e.get("source_sha256") == bench.source_sha() or e.get("kernel_sha") == ks, \
+                (name, workload, "PMC count of other kernel code: re-run tools/gpu_pmc.sh")
 
 
 def test_struct_layouts_match_header():
