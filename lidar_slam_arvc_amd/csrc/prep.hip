@@ -1580,46 +1580,6 @@ normals_kernel(const Seg *segs, const CloudDev *cd, NormalParams np,
 }
 
 
-// Sorts a workgroup's (key, value) pairs in LDS (sk, sv: PT_THREADS words each), keys descending;
-// every thread of the workgroup calls it with its own pair and gets the pair of its rank.
-__device__ __forceinline__ void wg_sort_desc(uint32_t *sk, uint32_t *sv, uint32_t &key, uint32_t &val) {
-    const int t = threadIdx.x;
-    sk[t] = key;
-    sv[t] = val;
-    __syncthreads();
-    for (int k = 2; k <= PT_THREADS; k <<= 1) {   // bitonic
-        for (int h = k >> 1; h > 0; h >>= 1) {
-            const int p = t ^ h;
-            if (p > t) {
-                const uint32_t a = sk[t], b = sk[p];
-                if ((t & k) == 0 ? a < b : a > b) {
-                    sk[t] = b;
-                    sk[p] = a;
-                    const uint32_t va = sv[t];
-                    sv[t] = sv[p];
-                    sv[p] = va;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    key = sk[t];
-    val = sv[t];
-    __syncthreads();
-}
-
-// The population of the cell holding qf (>= 1 for a point of the cloud): the walks' length scales
-// with it (the cell is the scale of the normals' ball).
-__device__ __forceinline__ uint32_t own_cell_count(const CloudDev &C, float4 qf) {
-    auto cc = [](float v, float o, float inv, int n) {
-        const int c = (int)floorf((v - o) * inv);
-        return c < 0 ? 0 : (c > n - 1 ? n - 1 : c);
-    };
-    const int l = lsm_cell_lin(C.nbx, C.nby, cc(qf.x, C.ox, C.inv_cell, C.nx),
-                               cc(qf.y, C.oy, C.inv_cell, C.ny), cc(qf.z, C.oz, C.inv_cell, C.nz));
-    return lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l);
-}
-
 // Split launch, first half: the points predicted sparse (NL_SPARSE, no LDS). Deferred points are
 // appended to their cloud's dense list dlist[geo.pt_off + ...] (wave-aggregated; the order of
 // the list does not matter: every point's computation is independent of the others).
@@ -1650,10 +1610,6 @@ __device__ __forceinline__ void wg_append(bool take, uint32_t j, uint32_t *list,
 #ifndef LSM_NSPARSE_WPE
 #define LSM_NSPARSE_WPE 8
 #endif
-// LSM_NSPARSE_SORT: each workgroup orders its points by their own cell's population
-#ifndef LSM_NSPARSE_SORT
-#define LSM_NSPARSE_SORT 0
-#endif
 #if LSM_NSPARSE_WPE > 0
 #define LSM_NSPARSE_ATTR __attribute__((amdgpu_waves_per_eu(LSM_NSPARSE_WPE)))
 #else
@@ -1667,22 +1623,8 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
     __shared__ uint32_t s_k[NSMALL_INLINE * PT_THREADS];
     const Seg s = segs[blockIdx.x];
     const CloudDev C = cd[s.cloud];
-#if LSM_NSPARSE_SORT
-    // the workgroup's points ordered by their own cell's population (as in the dense half), the
-    // keys sorted in s_f (not in use before the small-normal step)
-    static_assert(2 * PT_THREADS <= NSMALL_INLINE * PT_THREADS, "sort keys fit s_f");
-    uint32_t key = 0u, val = 0u;
-    if (s.start + int(threadIdx.x) < C.n) {
-        val = uint32_t(s.start) + threadIdx.x;
-        key = own_cell_count(C, lsm_ld(C.xyz, int(val)));
-    }
-    wg_sort_desc(s_f, s_f + PT_THREADS, key, val);
-    const int j = int(val);
-    const bool valid = key != 0u;
-#else
     const int j = s.start + threadIdx.x;
     const bool valid = j < C.n;
-#endif
     bool defer = false, small = false;
     int small_n = 0;
     if (valid) {
@@ -1707,10 +1649,6 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
 // Split launch, second half: one lane per entry of the clouds' dense lists (NL_DENSE), so the
 // truncated neighbourhoods run in full waves. The grid is the first half's (a cloud's list never
 // holds more entries than the cloud has points); workgroups past the list return at once.
-// LSM_NDENSE_SORT: each workgroup orders its dense-list entries by their own cell's population
-#ifndef LSM_NDENSE_SORT
-#define LSM_NDENSE_SORT 0
-#endif
 // LSM_NDENSE_WPE: waves per SIMD requested for the dense half (0: no request)
 #ifndef LSM_NDENSE_WPE
 #define LSM_NDENSE_WPE 0
@@ -1728,31 +1666,10 @@ normals_dense_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, No
     __shared__ uint32_t lds[PT_THREADS * HSTRIDE];
     const Seg s = segs[blockIdx.x];
     const uint32_t slot = uint32_t(s.start) + threadIdx.x;
-#if LSM_NDENSE_SORT
-    // A wave walks as long as its lane with the most neighbours. The workgroup's entries are
-    // sorted by their own cell's population (the scale of the 0.3 m ball: a proxy of the walk
-    // length) before the lanes take them, so each wave holds similar neighbourhoods; every point's
-    // computation is its own, so the order does not change any result.
-    const uint32_t cnt = dcnt[s.cloud];
-    if (uint32_t(s.start) >= cnt) return;   // the whole workgroup
-    const CloudDev C = cd[s.cloud];
-    const uint32_t off = geo[s.cloud].pt_off;
-    static_assert(2 * PT_THREADS <= PT_THREADS * HSTRIDE, "sort keys fit the lanes' rows");
-    uint32_t key = 0u, val = 0u;   // entries past the list: key 0, sorted last
-    if (slot < cnt) {
-        val = dlist[off + slot];
-        key = own_cell_count(C, lsm_ld(C.xyz, int(val)));
-    }
-    wg_sort_desc(lds, lds + PT_THREADS, key, val);   // the lanes' rows are not in use yet
-    const bool valid = key != 0u;
-    const int j = int(val);
-    if (!valid) return;
-#else
     if (slot >= dcnt[s.cloud]) return;
     const CloudDev C = cd[s.cloud];
     const uint32_t off = geo[s.cloud].pt_off;
     const int j = int(dlist[off + slot]);
-#endif
     const float4 q = lsm_ld(C.xyz, j);
     CumAcc acc{Cum{}, double(q.x), double(q.y), double(q.z), const_cast<float4 *>(C.nrm) + j,
                C.prior_ref ? C.prior_ref + C.perm[j] : nullptr};
