@@ -39,11 +39,12 @@ extern "C" {
 #define LSM_P2P 0     /* TransformationEstimationPointToPoint  (keyframe.py:246-248) */
 #define LSM_P2PLANE 1 /* TransformationEstimationPointToPlane  (keyframe.py:249-252) */
 
-/* want_normals = LSM_NORMALS_LAZY: the same normals as want_normals = 1, each computed when it
- * is first used. A P2Plane registration computes, pass by pass, only the normals of the target
- * points its correspondences reach (the others are never read); any other use of the normals
- * (download, FPFH, plane split, voxel_down_sample with normals) completes them first. The
- * values are bit-identical to the eager estimate_normals (keyframe.py:160-162). */
+/* want_normals = LSM_NORMALS_LAZY: the same normals as want_normals = 1, computed per keyframe
+ * when they are first used. A P2Plane registration computes all pending normals of its batch's
+ * targets before its first pass, in one launch over those clouds; clouds that are never a
+ * P2Plane target (loop-closure or multi-scale sources) never compute theirs. Any other use of
+ * the normals (download, FPFH, plane split, voxel_down_sample with normals) completes them
+ * first. The values are bit-identical to the eager estimate_normals (keyframe.py:160-162). */
 #define LSM_NORMALS_LAZY 2
 
 typedef struct lsm_ctx lsm_ctx;
@@ -219,9 +220,19 @@ int lsm_se3_prefix(const double *rel, int64_t n, double *out);
 
 /* Instrumentation ------------------------------------------------------------------------
  * With timing on, the library brackets every launch of the named kernel with HIP events on its
- * own stream and accumulates the durations. Kernel names: "nn" (correspondence search),
- * "nn_fallback", "accumulate", "solve", "normals", "normals_overflow", "filter", "grid".
- * algo_bytes: algorithmic bytes the kernel moved (SURVEY.md §8d model; nn only).
+ * own stream and accumulates the durations. Kernel names:
+ *   "filter", "voxel", "grid"          pre-processing (filter_radius_height, voxel_down_sample,
+ *                                      the cell-sorted layout)
+ *   "normals"                          estimate_normals in the pre-process (the split launch)
+ *   "normals_lazy"                     LSM_NORMALS_LAZY clouds' normals, computed by a P2Plane
+ *                                      registration or another first use
+ *   "nn", "nn_fallback"                the correspondence search and its fallback, per pass
+ *   "accumulate", "solve"              the JtJ / moment sums and the per-pair solve, per pass
+ *   "plane", "ransac", "fpfh", "feature_nn"   icp2planes and fpfh
+ * Aggregates: "nn_pass" (launches = correspondence passes; ms = "nn" + "nn_fallback" of those
+ * passes; algo_bytes = their SURVEY.md §8d bytes), and the counters "nn_queries",
+ * "nn_queries_first_pass", "nn_uncertified", "nn_pending", "nn_pending_first_pass" (counts in
+ * `launches`). algo_bytes: algorithmic bytes moved (SURVEY.md §8d model; "nn" and "nn_pass").
  * enable = 2 (statistics mode, slower): also count the neighbours of every normal computed
  * ("normals_neighbours", "normals_points" and "normals_truncated" in `launches`). */
 int lsm_set_timing(lsm_ctx *ctx, int32_t enable);

@@ -93,12 +93,16 @@ __device__ __forceinline__ bool better(float d2, int idx, float bd2, int bidx) {
     return d2 < bd2 || (d2 == bd2 && idx < bidx);
 }
 
+// T . p in f64 with ONE fixed rounding sequence (explicit fmas, no compiler contraction): the
+// certificate check recomputes a search's query point from the transform history and relies on
+// getting the search's point bit for bit, whichever call site (and inlining) computed it.
 __device__ __forceinline__ void transform_point(const double *T, float4 p, double &x, double &y,
                                                 double &z) {
+#pragma clang fp contract(off)
     const double px = p.x, py = p.y, pz = p.z;
-    x = T[0] * px + T[1] * py + T[2] * pz + T[3];
-    y = T[4] * px + T[5] * py + T[6] * pz + T[7];
-    z = T[8] * px + T[9] * py + T[10] * pz + T[11];
+    x = __builtin_fma(T[2], pz, __builtin_fma(T[1], py, __builtin_fma(T[0], px, T[3])));
+    y = __builtin_fma(T[6], pz, __builtin_fma(T[5], py, __builtin_fma(T[4], px, T[7])));
+    z = __builtin_fma(T[10], pz, __builtin_fma(T[9], py, __builtin_fma(T[8], px, T[11])));
 }
 
 // Running (nearest, second-nearest) over examined target points (the fallback's search state).
@@ -688,19 +692,22 @@ __device__ __forceinline__ void push_fallback(bool pending, int pair, int i, flo
     }
 }
 
-// Stability check of one query (passes >= 1). cert[g] = (q_s, rho): the f32 query point of the
-// search that found corr[g] (and alt[g], its second point, or -1) and that search's rho (a lower
-// bound on |q_s - t'| for every target point t' other than corr[g] and alt[g]; for every point
-// when corr[g] = -1). For this pass's query point q, every such point is at least rho - D away,
+// Stability check of one query (passes >= 1). corr[g] is the nearest neighbour the query's last
+// search found; rec[g] = (alt | spass << REC_SHIFT, rho) is that search's second point (REC_NONE:
+// none), the pass spass it ran in, and its rho (a lower bound on |q_s - t'| for every target
+// point t' other than corr[g] and alt; for every point when corr[g] = -1). q_s, the search's f32
+// query point, is not stored: it is recomputed from the pair's transform history (hist[spass],
+// written by the solve kernel) with transform_point's fixed rounding, so it is the search's point
+// bit for bit. For this pass's query point q, every such point is at least rho - D away,
 // D = |q - q_s| (triangle inequality, f64 of the f32 points, rounded up). The winner w of
-// corr[g] and alt[g] in the exact f32 (d2, index) order is certified when |q - w| (1 + 1e-5) + D
+// corr[g] and alt in the exact f32 (d2, index) order is certified when |q - w| (1 + 1e-5) + D
 // < rho, i.e. every other point is strictly farther even after the f32 rounding of the search's
-// squared distances (relative error < 1e-6); only a swap (alt[g] won) is written, cert keeps
-// the search's reference point. D is the direct displacement since the search, not a sum of
-// per-pass steps, so a pair that oscillates keeps its certificates. A query without a neighbour
-// stays without one while rho - D >= max_corr (1 + 1e-5); one whose neighbour left max_corr drops
-// it and is re-based at q. Returns false when the query must be searched; `m` is then its margin
-// for the search's rho.
+// squared distances (relative error < 1e-6); only a swap (alt won) is written, and the record
+// keeps the search's pass (so q_s stays the search's point). D is the direct displacement since
+// the search, not a sum of per-pass steps, so a pair that oscillates keeps its certificates. A
+// query without a neighbour stays without one while rho - D >= max_corr (1 + 1e-5); one whose
+// neighbour left max_corr drops it and is re-based at q. Returns false when the query must be
+// searched; `m` is then its margin for the search's rho.
 __device__ __forceinline__ float motion_margin(const PairState &P, const float4 s,
                                                const NNParams &prm);
 
@@ -1450,8 +1457,10 @@ solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NN
         P.Tp[k] = P.T[k];
         P.T[k] = T[k];
     }
-    double *h = hist + (size_t(blockIdx.x) * prm.hmax + pass + 1) * HIST_STRIDE;   // pass + 1's T
-    for (int k = 0; k < HIST_STRIDE; ++k) h[k] = T[k];
+    if (hist) {   // null when no pass checks certificates
+        double *h = hist + (size_t(blockIdx.x) * prm.hmax + pass + 1) * HIST_STRIDE;  // pass + 1's T
+        for (int k = 0; k < HIST_STRIDE; ++k) h[k] = T[k];
+    }
     P.iter = pass + 1;
     P.prev_fitness = fitness;
     P.prev_rmse = rmse;
@@ -1580,11 +1589,24 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int32_t *d_corr = (int32_t *)ctx->buf("i_corr", nsrc_tot * 4);
     int2 *d_rec = (int2 *)ctx->buf("i_rec", nsrc_tot * 8);
     // every pair's transform at every pass (the certificates' search points): slot 0 is the
-    // initial transform, slot k + 1 the one solve k leaves
+    // initial transform, slot k + 1 the one solve k leaves. The certificate record holds the
+    // search pass in 8 bits and alt in 24: beyond those bounds (or with LSM_NN_NOCERT) every pass
+    // searches every query, and no history is kept.
     const int hmax = max_iter + 2;
-    double *d_hist = (double *)ctx->buf("i_hist", size_t(npairs) * hmax * HIST_STRIDE * 8);
-    if (!d_hist) return LSM_ENOMEM;
-    hist_init_kernel<<<int((npairs + 255) / 256), 256, 0, st>>>(d_ps, int(npairs), hmax, d_hist);
+    int64_t max_tgt = 0;
+    for (int64_t k = 0; k < npairs; ++k) max_tgt = std::max<int64_t>(max_tgt, tgt[k]->n);
+    const bool nocert = lsm_knob("LSM_NN_NOCERT", 0) != 0.0 || hmax > 256 ||
+                        max_tgt >= int64_t(REC_NONE);
+    double *d_hist = nullptr;
+    if (!nocert) {
+        d_hist = (double *)ctx->buf("i_hist", size_t(npairs) * hmax * HIST_STRIDE * 8);
+        if (!d_hist) {
+            ctx->set_error("scratch allocation failed: i_hist");
+            return LSM_ENOMEM;
+        }
+        hist_init_kernel<<<int((npairs + 255) / 256), 256, 0, st>>>(d_ps, int(npairs), hmax,
+                                                                    d_hist);
+    }
     const uint32_t qcap = uint32_t(nsrc_tot);
     FallbackItem *d_q = (FallbackItem *)ctx->buf("i_queue", size_t(qcap) * sizeof(FallbackItem));
     double *d_part = (double *)ctx->buf("i_part", size_t(std::max(slot, 1)) * LSM_ACC * 8);
@@ -1659,7 +1681,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     const int64_t per0 = (total_blk + NXCD - 1) / NXCD;
     int grid = int(std::max<int64_t>(per0 * NXCD, NXCD));
     int32_t *h_poll = (int32_t *)ctx->host_pinned(size_t(ncnt) * 3 * 4);
-    if (!h_poll) return LSM_ENOMEM;
+    if (!h_poll) {
+        ctx->set_error("pinned allocation failed (icp poll words)");
+        return LSM_ENOMEM;
+    }
     // plan_kernel stores the poll words into this mapped pinned buffer (no copy dispatches)
     int32_t *d_poll = nullptr;
     std::memset(h_poll, 0xff, size_t(ncnt) * 3 * 4);
@@ -1683,12 +1708,6 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     // follows the first update, which moves the scans by centimetres to decimetres -- beyond
     // nearly every certificate -- so the check would only add its loads before the search
     const int CERT_FROM = std::max(1, int(lsm_knob("LSM_NN_CERT_FROM", 2)));
-    // (the certificate record holds the search pass in 8 bits and alt in 24: beyond those
-    // bounds every pass searches every query)
-    int64_t max_tgt = 0;
-    for (int64_t k = 0; k < npairs; ++k) max_tgt = std::max<int64_t>(max_tgt, tgt[k]->n);
-    const bool nocert = lsm_knob("LSM_NN_NOCERT", 0) != 0.0 || hmax > 256 ||
-                        max_tgt >= int64_t(REC_NONE);
     double ms0 = 0.0;
     for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
     unsigned long long *d_nst = nullptr;

@@ -707,8 +707,12 @@ __device__ __forceinline__ void cum_add_pt(Cum &c, float4 p, double qx, double q
 #endif
 constexpr int NSMALL = LSM_NSMALL;
 // the sparse half keeps the first members of each neighbourhood (LDS: 8 slots keep it at 8 waves
-// per SIMD), so it finishes small neighbourhoods of up to this many points without a second walk
-constexpr int NSMALL_INLINE = NSMALL < 8 ? NSMALL : 8;
+// per SIMD) and finishes every small neighbourhood from them without a second walk; there is no
+// other pass for the sparse half's small ones, so NSMALL may not exceed what it keeps
+constexpr int NSMALL_INLINE = NSMALL;
+static_assert(NSMALL >= 3 && NSMALL <= 8,
+              "the sparse half finishes neighbourhoods of 3..NSMALL points from the <= 8 members "
+              "its scan 1 keeps in LDS");
 
 // The normal of covariance A. prior (nullable): EstimateNormals on a cloud that already has
 // normals -- a zero normal keeps the prior one, and the new normal is flipped when it points
@@ -1637,9 +1641,8 @@ normals_sparse_kernel(const Seg *segs, const CloudDev *cd, const GridGeo *geo, N
         small = !defer && acc.c.n >= 3 && acc.c.n <= NSMALL_INLINE;
         small_n = acc.c.n;
     }
-    // a neighbourhood of at most NSMALL_INLINE points gets Open3D's arithmetic at once: scan 1
-    // kept its members (the batch's small-neighbourhood pass then takes the larger small ones,
-    // and the few the other paths marked)
+    // a neighbourhood of 3..NSMALL points gets Open3D's arithmetic at once from the members scan 1
+    // kept (the dense, refine and one-kernel paths walk their rare small ones again themselves)
     if (small) small_normal_from_list<PT_THREADS>(C, j, s_f + threadIdx.x, s_k + threadIdx.x, small_n);
     // one append per workgroup: its deferred points stay one run in cell order (the dense
     // half's waves then hold neighbouring points)

@@ -9,9 +9,13 @@ Two restatements: ``open3d_restated`` (NumPy/SciPy, the reference checker of the
 §8d's CPU baseline, timed by bench.py; tests/test_cpu_baseline.py checks it against the former).
 
 Pinning status:
-* filter, loop-closure candidate search, SE(3) host math: pinned bit-exactly against golden
-  vectors captured by importing the reference modules in the build container
-  (``tests/golden/make_golden.py``).
+* loop-closure candidates / triplets / triangle acceptance, SE(3) host math, ``sample_times``
+  and the EuRoC CSV schema: pinned bit-exactly against golden vectors captured by importing the
+  NumPy-only reference modules in the build container (``tests/golden/make_golden.py``).
+* filter_radius_height (keyframe.py:74-94): plain NumPy in the reference, but keyframe.py imports
+  open3d at module level and cannot be imported here, so no vectors were captured from it; the
+  restatement follows its mask line by line (strict inequalities, order kept) and is pinned by
+  known-answer tests at the strict edges, NaN and inf (tests/test_oracle_kats.py).
 * voxel down-sample, hybrid-kNN normals, ICP (P2P / P2Plane): the arithmetic lives in Open3D, which
   is un-vendored and absent here, so these are *parity unpinned* by reference
   fixtures. They are restated from Open3D's published algorithm and pinned by known-answer tests

@@ -11,7 +11,8 @@ from oracle import open3d_restated as O
 
 def test_filter_strict_bounds():
     p = np.array([[0.5, 0, 0], [0.50001, 0, 0], [35, 0, 0], [34.9999, 0, 0], [1, 1, -1.0],
-                  [1, 1, -0.999], [1, 1, 50.0], [1, 1, 49.99], [np.nan, 1, 1]])
+                  [1, 1, -0.999], [1, 1, 50.0], [1, 1, 49.99], [np.nan, 1, 1], [np.inf, 0, 0],
+                  [1, 1, np.inf], [1, 1, -np.inf], [1, np.nan, 0]])
     out = O.filter_radius_height(p)
     assert out.tolist() == [[0.50001, 0, 0], [34.9999, 0, 0], [1, 1, -0.999], [1, 1, 49.99]]
 

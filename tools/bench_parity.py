@@ -1,19 +1,26 @@
-"""Headline-workload parity: every pair of bench.py's C3 sequence (seed 3, 2000 HDL-64 keyframes,
-1999 consecutive P2Plane pairs) through the GPU path and through the f64 C++/OpenMP CPU
-implementation of the same path (oracle/cpu/lsm_cpu.cpp, the checker), then a summary.
+"""Bench-workload parity: every pair of one of bench.py's batches through the GPU path and
+through the f64 C++/OpenMP CPU implementation of the same path (oracle/cpu/lsm_cpu.cpp, the
+checker), then a summary. Workloads (``--workload``, the same names and seeds as bench.py):
 
-Reference semantics: keyframe.py:246-252 (registration_icp, P2Plane, max_corr 10 m, Open3D's
-default criteria) on the pairs of run_scanmatcher.py:196-213 (each pair seeded with its
-odometry prior).
+* hdl64_seq (C3): the seed-3 sequence, 2000 HDL-64 keyframes, 1999 consecutive P2Plane pairs --
+  keyframe.py:246-252 (registration_icp, P2Plane, max_corr 10 m, Open3D's default criteria) on
+  the pairs of run_scanmatcher.py:196-213, each seeded with its odometry prior;
+* loop_closure (C4): rank 0's 512 independent seed-4 revisit pairs (the loop-closure ICPs of
+  loopclosing.py:80-99 / 163-180, scaled to a batch), both keyframes pre-processed, P2Plane,
+  init = the perturbed revisit pose; the GPU side runs them as bench.py does (lazy normals);
+* ouster_multiscale (C5): rank 0's 512 consecutive pairs of the seed-5 Ouster-128 sequence
+  through the 3-scale chain (filter, voxel 0.4 / 0.2 / 0.1 m -- keyframe.py:150-151 / 158-159 --,
+  normals, P2Plane ICP with max_corr 2 / 1 / 0.5 m; lidar_slam_arvc_amd/multiscale.py); every
+  stage is compared.
 
 Two modes:
 
-  python tools/bench_parity.py --make-cpu OUT.npz
+  python tools/bench_parity.py [--workload W] --make-cpu OUT.npz
       CPU side only (any host; all cores): writes the oracle's per-pair results together with a
       SHA-256 of the generated sequence, so a GPU run elsewhere can prove it saw the same data.
 
-  python tools/bench_parity.py [--cpu FIXTURE.npz | --cpu-live] [--out SUMMARY.json]
-      GPU side (the bench's own batch: pre-process all 2000 keyframes, one 1999-pair ICP batch),
+  python tools/bench_parity.py [--workload W] [--cpu FIXTURE.npz | --cpu-live] [--out SUMMARY.json]
+      GPU side (the bench's own batch: pre-process every keyframe, one ICP batch per stage),
       compared against the fixture (or against the C++ oracle run live on this host's cores).
 
 Summary (JSON): pairs within north_star's tolerance (|dR| <= 1e-4, |dt| <= 1e-3 m), the worst
@@ -38,10 +45,32 @@ TOL_R, TOL_T = 1e-4, 1e-3
 MAX_ITER = 30
 
 
-def sequence(P: int, seed: int):
+WORKLOADS = {   # name -> (default pairs, default seed, fixture under tests/golden)
+    "hdl64_seq": (1999, 3, "seed3_seq_cpu_oracle.npz"),
+    "loop_closure": (512, 4, "seed4_loop_cpu_oracle.npz"),
+    "ouster_multiscale": (512, 5, "seed5_ouster_cpu_oracle.npz"),
+}
+
+
+def sequence(P: int, seed: int, workload: str = "hdl64_seq", processes: int = 0):
+    """bench.py's rank-0 data of `workload` (first_index 0). loop_closure: a Sequence whose scans
+    are the P targets then the P sources and whose priors are the P initial guesses (bench.py's
+    layout)."""
     from lidar_slam_arvc_amd import synthetic
-    procs = max(1, min(16, len(os.sched_getaffinity(0))))
-    return synthetic.make_sequence(P + 1, seed=seed, model=synthetic.HDL64, processes=procs)
+    procs = processes or max(1, min(16, len(os.sched_getaffinity(0))))
+    if workload == "loop_closure":
+        ps = synthetic.make_revisit_pairs(P, seed=seed, model=synthetic.HDL64, processes=procs)
+        return synthetic.Sequence(ps.targets + ps.sources, np.zeros((0, 4, 4)), ps.init)
+    model = synthetic.OUSTER128 if workload == "ouster_multiscale" else synthetic.HDL64
+    return synthetic.make_sequence(P + 1, seed=seed, model=model, processes=procs)
+
+
+def pair_clouds(seq, workload: str):
+    """(source index, target index) of every pair into seq.scans, in bench.py's order."""
+    if workload == "loop_closure":
+        P = len(seq.priors)
+        return [(P + k, k) for k in range(P)]
+    return [(k + 1, k) for k in range(len(seq.scans) - 1)]
 
 
 def seq_hash(seq) -> str:
@@ -52,10 +81,56 @@ def seq_hash(seq) -> str:
     return h.hexdigest()
 
 
-def run_cpu(seq, threads: int, log=print):
-    """The C++ oracle on every pair: filter + normals per keyframe, then registration_icp."""
+def run_cpu_multiscale(seq, threads: int, log=print):
+    """C5: the C++ oracle's 3-scale chain on every consecutive pair (cpu_ref.registration_multiscale:
+    filter, then per scale voxel + normals of the target + ICP from the previous stage's T).
+    Results per stage: arrays with a leading stage axis."""
     from oracle import cpu_ref as C
     C.set_threads(threads)
+    P = len(seq.scans) - 1
+    S = 3
+    T = np.zeros((S, P, 4, 4))
+    fit, rmse = np.zeros((S, P)), np.zeros((S, P))
+    iters, ncorr = np.zeros((S, P), np.int32), np.zeros((S, P), np.int64)
+    t0 = last = time.time()
+    for k in range(P):
+        for s, r in enumerate(C.registration_multiscale(seq.scans[k + 1], seq.scans[k],
+                                                        seq.priors[k])):
+            T[s, k] = r["transformation"]
+            fit[s, k], rmse[s, k] = r["fitness"], r["inlier_rmse"]
+            iters[s, k], ncorr[s, k] = r["iterations"], r["n_corr"]
+        if time.time() - last > 30:
+            last = time.time()
+            log(f"cpu: {k + 1}/{P} pairs, {last - t0:.0f} s", flush=True)
+    return dict(transformation=T, fitness=fit, inlier_rmse=rmse, iterations=iters,
+                n_corr=ncorr, seconds=time.time() - t0, threads=threads)
+
+
+def run_cpu(seq, threads: int, log=print, workload: str = "hdl64_seq"):
+    """The C++ oracle on every pair: filter + normals per keyframe, then registration_icp."""
+    from oracle import cpu_ref as C
+    if workload == "ouster_multiscale":
+        return run_cpu_multiscale(seq, threads, log)
+    C.set_threads(threads)
+    if workload == "loop_closure":
+        P = len(seq.priors)
+        T = np.zeros((P, 4, 4))
+        fit, rmse = np.zeros(P), np.zeros(P)
+        iters, ncorr = np.zeros(P, np.int32), np.zeros(P, np.int64)
+        t0 = last = time.time()
+        for k, (si, ti) in enumerate(pair_clouds(seq, workload)):
+            tp = C.filter_radius_height(seq.scans[ti])
+            sp = C.filter_radius_height(seq.scans[si])
+            r = C.registration_icp(sp, tp, 10.0, seq.priors[k], "p2plane",
+                                   C.estimate_normals(tp))
+            T[k] = r["transformation"]
+            fit[k], rmse[k] = r["fitness"], r["inlier_rmse"]
+            iters[k], ncorr[k] = r["iterations"], r["n_corr"]
+            if time.time() - last > 30:
+                last = time.time()
+                log(f"cpu: {k + 1}/{P} pairs, {last - t0:.0f} s", flush=True)
+        return dict(transformation=T, fitness=fit, inlier_rmse=rmse, iterations=iters,
+                    n_corr=ncorr, seconds=time.time() - t0, threads=threads)
     P = len(seq.scans) - 1
     T = np.zeros((P, 4, 4))
     fit, rmse = np.zeros(P), np.zeros(P)
@@ -81,14 +156,28 @@ def run_cpu(seq, threads: int, log=print):
                 n_corr=ncorr, seconds=time.time() - t0, threads=threads)
 
 
-def run_gpu(seq):
-    """The bench's batch; returns (results, device, handles) -- the handles stay resident for
-    explain()."""
+def run_gpu(seq, workload: str = "hdl64_seq", dev=None):
+    """The bench's batch, as bench.py's step runs it (normals: eager for hdl64_seq, lazy for the
+    other two); returns (results, device, handles) -- the handles stay resident for explain().
+    ouster_multiscale: arrays with a leading stage axis (the handles are the raw scans)."""
     from lidar_slam_arvc_amd import _lib
-    dev = _lib.device(0)
+    dev = dev or _lib.device(0)
     ids = [dev.upload(s) for s in seq.scans]
-    dev.preprocess(ids, _lib.prep_params())
-    res = dev.icp_batch_arrays(ids[1:], ids[:-1], seq.priors, _lib.icp_params())
+    if workload == "ouster_multiscale":
+        from lidar_slam_arvc_amd.multiscale import MultiScaleSet
+        P = len(seq.scans) - 1
+        with MultiScaleSet(dev, ids) as ms:
+            ms.preprocess(want_normals="lazy")
+            stages = ms.register(list(range(1, P + 1)), list(range(P)), seq.priors, arrays=True)
+        res = {k: np.stack([np.asarray(st[k]) for st in stages]) for k in stages[0]}
+        return res, dev, ids
+    if workload == "loop_closure":
+        P = len(seq.priors)
+        dev.preprocess(ids, _lib.prep_params(want_normals="lazy"))
+        res = dev.icp_batch_arrays(ids[P:], ids[:P], seq.priors, _lib.icp_params())
+    else:
+        dev.preprocess(ids, _lib.prep_params())
+        res = dev.icp_batch_arrays(ids[1:], ids[:-1], seq.priors, _lib.icp_params())
     return {k: np.array(v) for k, v in res.items()}, dev, ids
 
 
@@ -180,40 +269,62 @@ def compare(gpu, cpu) -> dict:
     }
 
 
+def compare_workload(gpu, cpu, workload: str) -> dict:
+    """compare() of the final results; ouster_multiscale: of the last stage, plus every stage's
+    within-tolerance count (each stage is the reference's single-scale operator)."""
+    if workload != "ouster_multiscale":
+        return compare(gpu, cpu)
+    S = np.asarray(cpu["transformation"]).shape[0]
+    keys = ("transformation", "fitness", "inlier_rmse", "iterations")
+    out = compare({k: np.asarray(gpu[k])[S - 1] for k in keys},
+                  {k: np.asarray(cpu[k])[S - 1] for k in keys})
+    out["stages"] = [{"stage": s, **{k: v for k, v in compare(
+        {k: np.asarray(gpu[k])[s] for k in keys},
+        {k: np.asarray(cpu[k])[s] for k in keys}).items()
+        if k in ("pairs", "within_tolerance", "converged_both", "iterations_equal",
+                 "worst_converged", "outside_tolerance_converged")}} for s in range(S)]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--pairs", type=int, default=1999)
-    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--workload", default="hdl64_seq", choices=sorted(WORKLOADS))
+    ap.add_argument("--pairs", type=int, default=0, help="0: the workload's bench.py default")
+    ap.add_argument("--seed", type=int, default=-1, help="-1: the workload's bench.py default")
     ap.add_argument("--make-cpu", default="", help="CPU side only: write the oracle fixture here")
-    ap.add_argument("--cpu", default=os.path.join(ROOT, "tests", "golden",
-                                                  "seed3_seq_cpu_oracle.npz"))
+    ap.add_argument("--cpu", default="", help="fixture (default: tests/golden/<workload's>)")
     ap.add_argument("--cpu-live", action="store_true",
                     help="run the C++ oracle here instead of reading the fixture")
     ap.add_argument("--threads", type=int, default=0, help="0: every core this process may use")
     ap.add_argument("--out", default="")
     ap.add_argument("--explain", action="store_true",
-                    help="three-way analysis (GPU / C++ / NumPy oracle, normals) of every pair "
-                         "outside the bar")
+                    help="hdl64_seq: three-way analysis (GPU / C++ / NumPy oracle, normals) of "
+                         "every pair outside the bar")
     ap.add_argument("--save-gpu", default="", help="write the GPU's per-pair results here")
     args = ap.parse_args()
     threads = args.threads or len(os.sched_getaffinity(0))
+    P0, seed0, fixture = WORKLOADS[args.workload]
+    args.pairs = args.pairs or P0
+    args.seed = args.seed if args.seed >= 0 else seed0
+    args.cpu = args.cpu or os.path.join(ROOT, "tests", "golden", fixture)
 
     t0 = time.time()
-    seq = sequence(args.pairs, args.seed)
+    seq = sequence(args.pairs, args.seed, args.workload)
     digest = seq_hash(seq)
-    print(f"sequence: {len(seq.scans)} keyframes in {time.time() - t0:.1f} s, sha256 {digest}",
-          flush=True)
+    print(f"{args.workload}: {len(seq.scans)} clouds in {time.time() - t0:.1f} s, "
+          f"sha256 {digest}", flush=True)
     if args.make_cpu:
-        cpu = run_cpu(seq, threads)
-        np.savez_compressed(args.make_cpu, sha256=digest, seed=args.seed, **cpu)
+        cpu = run_cpu(seq, threads, workload=args.workload)
+        np.savez_compressed(args.make_cpu, sha256=digest, seed=args.seed,
+                            workload=args.workload, **cpu)
         print(f"cpu oracle: {args.pairs} pairs in {cpu['seconds']:.1f} s on {threads} threads "
               f"-> {args.make_cpu}", flush=True)
         return
 
-    gpu, dev, ids = run_gpu(seq)
+    gpu, dev, ids = run_gpu(seq, args.workload)
     print(f"gpu: {args.pairs} pairs done", flush=True)
     if args.cpu_live:
-        cpu = run_cpu(seq, threads)
+        cpu = run_cpu(seq, threads, workload=args.workload)
         src = f"C++ oracle run live on {threads} threads ({cpu['seconds']:.1f} s)"
     else:
         z = np.load(args.cpu)
@@ -221,11 +332,11 @@ def main():
             raise SystemExit(f"fixture {args.cpu} was made from a different sequence")
         cpu = {k: z[k] for k in z.files}
         src = (f"{os.path.relpath(args.cpu, ROOT)} (C++ oracle, {int(z['threads'])} threads, "
-               f"{float(z['seconds']):.0f} s; same sequence sha256)")
-    summary = compare(gpu, cpu)
-    summary = {"workload": f"hdl64_64k_p2plane_seq seed {args.seed}, {args.pairs} pairs",
+               f"{float(z['seconds']):.0f} s; same clouds' sha256)")
+    summary = compare_workload(gpu, cpu, args.workload)
+    summary = {"workload": f"{args.workload} seed {args.seed}, {args.pairs} pairs",
                "sequence_sha256": digest, "checker": src, **summary}
-    if args.explain:
+    if args.explain and args.workload == "hdl64_seq":
         P = len(cpu["transformation"])
         Tg = np.asarray(gpu["transformation"]).reshape(P, 4, 4)
         Tc = np.asarray(cpu["transformation"]).reshape(P, 4, 4)
