@@ -150,6 +150,10 @@ def parse():
     ap.add_argument("--no-c1", action="store_true",
                     help="skip the lines of configs C1 (8k-point P2P pairs) and C2 (one 64k "
                          "P2Plane pair), CPU and GPU")
+    ap.add_argument("--no-c45", action="store_true",
+                    help="skip the c4 / c5 blocks (configs C4 loop-closure pairs and C5 Ouster-128 "
+                         "multi-scale, 512 pairs per GPU each, timed like the main line); "
+                         "profiling runs of one workload use it")
     ap.add_argument("--grid-cell", type=float, default=0.0, help="spatial grid cell (m); 0 = library default")
     ap.add_argument("--grid-cell-scales", default="",
                     help="ouster_multiscale: comma-separated grid cell per voxel scale (overrides --grid-cell)")
@@ -349,27 +353,21 @@ def c2_line(dev, seq, threads: int):
             "cpu_baseline": cpu, "cpu_ms_per_pair": round(1e3 / cpu["value"], 1)}
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    from lidar_slam_arvc_amd import synthetic
+WORKLOAD_DEFAULTS = {   # bench workload -> (pairs per GPU, seed, LiDAR model name, normals mode)
+    "hdl64_seq": (1999, 3, "HDL64", "eager"),           # C3 (and C2's scans)
+    "loop_closure": (512, 4, "HDL64", "lazy"),          # C4: 4096 pairs over 8 GPUs
+    "ouster_multiscale": (512, 5, "OUSTER128", "lazy"),  # C5
+}
 
-    ouster = args.workload == "ouster_multiscale"
-    loop = args.workload == "loop_closure"
-    if args.normals == "auto":
-        args.normals = "lazy" if (ouster or loop) else "eager"
-    P = args.pairs_per_gpu or (512 if ouster else (512 if loop else 1999))
-    first = rank * P
-    model = synthetic.OUSTER128 if ouster else synthetic.HDL64
-    seed = args.seed if args.seed >= 0 else (5 if ouster else (4 if loop else 3))
-    # synthetic scans first, in forked worker processes: nothing in this process has touched the
-    # GPU yet (a fork after HIP initialisation is not safe)
-    procs = max(1, min(8, os.cpu_count() or 1))
-    tag = f"{args.workload}_{P}_{seed}_{model.rings}x{model.azimuths}_{first}"
-    if loop:
-        # C4: every rank owns P independent revisit pairs (its own targets and sources)
+
+def make_data(workload: str, P: int, seed: int, first: int, procs: int, cache: str = ""):
+    """The rank's synthetic data of `workload` (forked ray-cast workers: call before the GPU is
+    touched). loop_closure: scans = the P targets then the P sources, priors = the P initial
+    guesses; otherwise P + 1 consecutive keyframes of one sequence."""
+    from lidar_slam_arvc_amd import synthetic
+    model = getattr(synthetic, WORKLOAD_DEFAULTS[workload][2])
+    tag = f"{workload}_{P}_{seed}_{model.rings}x{model.azimuths}_{first}"
+    if workload == "loop_closure":
         def make():
             ps = synthetic.make_revisit_pairs(P, seed=seed, model=model, first_index=first,
                                               processes=procs)
@@ -378,59 +376,40 @@ def main():
         def make():
             return synthetic.make_sequence(P + 1, seed=seed, model=model, first_index=first,
                                            processes=procs)
-    seq = load_or_make(args.seq_cache, tag, make)
-    c1 = c2 = None
-    do_cpu = world == 1 and not args.no_cpu_baseline
-    if do_cpu and not args.no_c1:
-        # C1: 8k-point (16 x 512 ray) P2P pairs, seed 1 -- the reference's CPU-runnable case
-        c1 = synthetic.make_sequence(C1_PAIRS + 1, seed=1, model=synthetic.VLP16_8K,
-                                     processes=procs)
-        # C2: one 64k HDL-64 pair, seed 2
-        c2 = synthetic.make_sequence(2, seed=2, model=synthetic.HDL64, processes=procs)
-    cpu_threads = args.cpu_threads or usable_cores()
-    # the kernel hashes spawn llvm-objdump: before this process touches the GPU (every rank: the
-    # normals' PMC lookup runs on all of them)
-    for kernels in PMC_KERNELS.values():
-        kernel_sha(tuple(kernels))
-    _GPU_STARTED[0] = True
+    return load_or_make(cache, tag, make)
 
+
+def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda, normals,
+                 streams=1, grid_cell=0.0, grid_cells=None, do_cpu=False, cpu_threads=1,
+                 cpu_sample=0):
+    """Upload `seq`, run W untimed and K timed steps of `workload` (barrier + synchronize on both
+    sides, max over ranks) and return (rank 0) its bench line without the top-level extras:
+    metric, value, config, roofline, roofline_normals, cpu_baseline, breakdown. Every rank must
+    call it (the steps' collectives)."""
+    from lidar_slam_arvc_amd import _lib
+    from lidar_slam_arvc_amd.distributed import compose_global_sharded, gather_pair_results
     import torch
     import torch.distributed as dist
 
-    # --share-gpu (a rehearsal of the N-rank path on a one-GPU box): every rank on device 0,
-    # collectives over gloo on host tensors; otherwise one GPU per rank and RCCL over xGMI
-    gpu = 0 if args.share_gpu else local
-    torch.cuda.set_device(gpu)
-    group = None
-    if world > 1:
-        if args.share_gpu:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        group = dist.group.WORLD
-
-    from lidar_slam_arvc_amd import _lib
-    from lidar_slam_arvc_amd.distributed import compose_global_sharded, gather_pair_results
-
+    ouster = workload == "ouster_multiscale"
+    loop = workload == "loop_closure"
+    first = rank * P
     extra_ids = []                                   # (context, handle) of extra runs
-    devs = [None]
     dev = _lib.device(gpu)
     ids = [dev.upload(s) for s in seq.scans]        # raw scans resident in HBM
+    devs = [dev]
     want_normals = args.method == "p2plane"
     # pre-process normals mode: "lazy" computes only the target normals the registration reads
-    wn_mode = ("lazy" if args.normals == "lazy" else True) if want_normals else False
-    cuda = torch.device("cpu") if args.share_gpu else torch.device("cuda", local)   # collectives
+    wn_mode = ("lazy" if normals == "lazy" else True) if want_normals else False
     ms = None
+    S = 1
     if ouster:
         from lidar_slam_arvc_amd.multiscale import MultiScaleSet
         ms = MultiScaleSet(dev, ids)                 # per-scale device clones, made once
-        grid_cells = ([float(c) for c in args.grid_cell_scales.split(",")]
-                      if args.grid_cell_scales else None)
-
         n_fine = []   # points per scan at the finest scale: the same every step, read once
 
         def step():
-            ms.preprocess(want_normals=wn_mode, grid_cell=args.grid_cell, grid_cells=grid_cells)
+            ms.preprocess(want_normals=wn_mode, grid_cell=grid_cell, grid_cells=grid_cells)
             stages = ms.register(list(range(1, P + 1)), list(range(P)), seq.priors,
                                  method=args.method, arrays=True)
             res = stages[-1]
@@ -439,7 +418,7 @@ def main():
                 n_fine.extend(dev.info(h)[1] for h in ms.handles[-1])
             return n_fine, res
     elif loop:
-        prep = _lib.prep_params(want_normals=wn_mode, grid_cell=args.grid_cell)
+        prep = _lib.prep_params(want_normals=wn_mode, grid_cell=grid_cell)
         icp = _lib.icp_params(method=args.method)
 
         def step():
@@ -451,9 +430,9 @@ def main():
                                     device=cuda)
             return n, res
     else:
-        prep = _lib.prep_params(want_normals=wn_mode, grid_cell=args.grid_cell)
+        prep = _lib.prep_params(want_normals=wn_mode, grid_cell=grid_cell)
         icp = _lib.icp_params(method=args.method)
-        S = max(1, min(args.streams, P))
+        S = max(1, min(streams, P))
         cut = [round(k * P / S) for k in range(S + 1)]          # pair runs [cut[s], cut[s+1])
         devs = [dev] + [_lib.Device(gpu) for _ in range(S - 1)]
         # run s owns keyframes cut[s] .. cut[s+1] (the shared end keyframe is in both runs)
@@ -494,188 +473,278 @@ def main():
             compose_global_sharded(rel, group=group, device=cuda)
             return n, res
 
-    for _ in range(args.warmup):
-        step()
-    devs = [d for d in devs if d is not None] or [dev]
-    for d in devs:
-        d.reset_stats()
-        d.set_timing(True)
-    if group is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    last = None
-    for _ in range(args.steps):
-        last = step()
-    torch.cuda.synchronize()
-    if group is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    for d in devs:
-        d.set_timing(False)
-    if group is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=cuda)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
-    def kstats(name):   # summed over the contexts (their kernels may overlap in time)
-        tot = {"launches": 0, "ms": 0.0, "algo_bytes": 0.0}
-        for d in devs:
-            st = d.kernel_stats(name)
-            for key in tot:
-                tot[key] += st[key]
-        return tot
-
-    stats = {k: kstats(k) for k in KERNELS}
-    nn = kstats("nn_pass")   # check + search + fallback of every ICP pass
-    cnt = {k: kstats(k)["launches"] for k in ("nn_uncertified", "nn_queries",
-                                              "nn_queries_first_pass", "nn_pending",
-                                              "nn_pending_first_pass")}
-    roof_n = None
-    norm_ms = stats["normals"]["ms"] + stats["normals_lazy"]["ms"]   # every normals launch
-    if want_normals and norm_ms > 0 and len(devs) == 1:
-        # neighbourhood sizes of the normals one step computes: one more (untimed) step in
-        # statistics mode (every rank runs it: the step's collectives need all ranks)
-        d0 = devs[0]
-        d0.reset_stats()
-        d0.set_timing(True, statistics=True)
-        try:
+    try:
+        for _ in range(args.warmup):
             step()
-        finally:
-            d0.set_timing(False)
-        nb = d0.kernel_stats("normals_neighbours")["launches"]
-        npts = d0.kernel_stats("normals_points")["launches"]
-        step_s = norm_ms / args.steps * 1e-3
-        flops = 18.0 * nb + 150.0 * npts
-        valu, valu_k = None, None
-        # PMC count of the same workload and normals mode (profiles/normals_valu.json)
-        vj, v_why = pmc_entry("normals_valu.json", args.workload, P, args.normals)
-        if vj:
-            valu = vj.get("valu_per_step")
-            valu_k = {k: v.get("SQ_INSTS_VALU")
-                      for k, v in vj.get("per_kernel_per_step", {}).items()}
-        ach = valu / step_s / 1e9 if valu else None
-        roof_n = {"bound": "valu", "kernel": "normals_sparse_kernel + normals_dense_kernel + "
-                                             "normals_refine_kernel (the split launch; " +
-                                             ("each keyframe's normals when it is first a P2Plane "
-                                              "target" if args.normals == "lazy" else
-                                              "every keyframe, once per step") +
-                                             "): hybrid kNN-300 / r 0.3 m",
-                  "mode": args.normals, "unit": "G wave-instructions/s",
-                  "valu_source": "profiles/normals_valu.json" if vj else v_why,
-                  "achieved": round(ach, 2) if ach else None, "peak": VALU_ISSUE_PEAK_G,
-                  "frac": round(ach / VALU_ISSUE_PEAK_G, 5) if ach else None,
-                  "valu_instructions_per_step": valu,
-                  "valu_instructions_per_kernel": valu_k,
-                  "ms_per_step": round(step_s * 1e3, 4),
-                  "launches_per_step": (stats["normals"]["launches"] +
-                                        stats["normals_lazy"]["launches"]) / args.steps,
-                  "flops": {"unit": "TFLOP/s", "achieved": round(flops / step_s / 1e12, 4),
-                            "peak": FP32_VALU_PEAK_TFLOPS,
-                            "frac": round(flops / step_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 6),
-                            "flops_per_step": flops,
-                            "model": "SURVEY.md 8d: 18 FLOP per neighbour (9 cumulant FMAs, "
-                                     "computed in f64) + 150 per point (covariance, "
-                                     "FastEigen3x3); neighbourhood sizes counted on the device",
-                            "normals_per_step": npts,
-                            "neighbours_per_normal": round(nb / max(npts, 1), 3)}}
+        for d in devs:
+            d.reset_stats()
+            d.set_timing(True)
+        if group is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        last = None
+        for _ in range(args.steps):
+            last = step()
+        torch.cuda.synchronize()
+        if group is not None:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        for d in devs:
+            d.set_timing(False)
+        if group is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device=cuda)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+
+        def kstats(name):   # summed over the contexts (their kernels may overlap in time)
+            tot = {"launches": 0, "ms": 0.0, "algo_bytes": 0.0}
+            for d in devs:
+                st = d.kernel_stats(name)
+                for key in tot:
+                    tot[key] += st[key]
+            return tot
+
+        stats = {k: kstats(k) for k in KERNELS}
+        nn = kstats("nn_pass")   # check + search + fallback of every ICP pass
+        cnt = {k: kstats(k)["launches"] for k in ("nn_uncertified", "nn_queries",
+                                                  "nn_queries_first_pass", "nn_pending",
+                                                  "nn_pending_first_pass")}
+        roof_n = None
+        norm_ms = stats["normals"]["ms"] + stats["normals_lazy"]["ms"]   # every normals launch
+        if want_normals and norm_ms > 0 and len(devs) == 1:
+            # neighbourhood sizes of the normals one step computes: one more (untimed) step in
+            # statistics mode (every rank runs it: the step's collectives need all ranks)
+            d0 = devs[0]
+            d0.reset_stats()
+            d0.set_timing(True, statistics=True)
+            try:
+                step()
+            finally:
+                d0.set_timing(False)
+            nb = d0.kernel_stats("normals_neighbours")["launches"]
+            npts = d0.kernel_stats("normals_points")["launches"]
+            step_s = norm_ms / args.steps * 1e-3
+            flops = 18.0 * nb + 150.0 * npts
+            valu, valu_k = None, None
+            # PMC count of the same workload and normals mode (profiles/normals_valu.json)
+            vj, v_why = pmc_entry("normals_valu.json", workload, P, normals)
+            if vj:
+                valu = vj.get("valu_per_step")
+                valu_k = {k: v.get("SQ_INSTS_VALU")
+                          for k, v in vj.get("per_kernel_per_step", {}).items()}
+            ach = valu / step_s / 1e9 if valu else None
+            roof_n = {"bound": "valu", "kernel": "normals_sparse_kernel + normals_dense_kernel + "
+                                                 "normals_refine_kernel (the split launch; " +
+                                                 ("each keyframe's normals when it is first a "
+                                                  "P2Plane target" if normals == "lazy" else
+                                                  "every keyframe, once per step") +
+                                                 "): hybrid kNN-300 / r 0.3 m",
+                      "mode": normals, "unit": "G wave-instructions/s",
+                      "valu_source": "profiles/normals_valu.json" if vj else v_why,
+                      "achieved": round(ach, 2) if ach else None, "peak": VALU_ISSUE_PEAK_G,
+                      "frac": round(ach / VALU_ISSUE_PEAK_G, 5) if ach else None,
+                      "valu_instructions_per_step": valu,
+                      "valu_instructions_per_kernel": valu_k,
+                      "ms_per_step": round(step_s * 1e3, 4),
+                      "launches_per_step": (stats["normals"]["launches"] +
+                                            stats["normals_lazy"]["launches"]) / args.steps,
+                      "flops": {"unit": "TFLOP/s", "achieved": round(flops / step_s / 1e12, 4),
+                                "peak": FP32_VALU_PEAK_TFLOPS,
+                                "frac": round(flops / step_s / 1e12 / FP32_VALU_PEAK_TFLOPS, 6),
+                                "flops_per_step": flops,
+                                "model": "SURVEY.md 8d: 18 FLOP per neighbour (9 cumulant FMAs, "
+                                         "computed in f64) + 150 per point (covariance, "
+                                         "FastEigen3x3); neighbourhood sizes counted on the "
+                                         "device",
+                                "normals_per_step": npts,
+                                "neighbours_per_normal": round(nb / max(npts, 1), 3)}}
+    finally:
+        if ms is not None:
+            ms.release()
+        for i in ids:
+            dev.release(i)
+        for d, h in extra_ids:
+            d.release(h)
+        for d in devs[1:]:
+            d.close()
 
     n_pts, res = last
-    iters = [r["iterations"] for r in res] if isinstance(res, list) else list(res["iterations"])
-    out = None
+    iters = list(res["iterations"])
+    if rank != 0:
+        return None
+    achieved = nn["algo_bytes"] / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0
+    # PMC traffic of the same workload (profiles/nn_traffic.json, tools/pmc_nn.sh)
+    tj, t_why = pmc_entry("nn_traffic.json", workload, P)
+    traffic = tj.get("hbm_bytes_per_launch") if tj else None
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_source": "profiles/nn_traffic.json" if tj else t_why,
+            "traffic_over_algorithmic": (round(traffic / (nn["algo_bytes"] /
+                                                          max(nn["launches"], 1)), 3)
+                                         if traffic and nn["algo_bytes"] else None),
+            "kernel": "correspondence pass: nn_kernel (stability check + box search) + "
+                      "nn_fallback",
+            "algo_bytes_per_launch": nn["algo_bytes"] / max(nn["launches"], 1),
+            "avg_launch_ms": nn["ms"] / max(nn["launches"], 1),
+            "launches": nn["launches"],
+            "per_kernel_ms_per_pass": {k: round(stats[k]["ms"] / max(nn["launches"], 1), 5)
+                                       for k in ("nn", "nn_fallback")}}
+    cpu = None
+    if do_cpu:
+        ns = cpu_sample or (32 if ouster else (72 if loop else 144))
+        ns = max(1, min(ns, P))
+        if ouster:
+            cpu = cpu_baseline_multiscale(seq, ns, args.method, cpu_threads)
+        elif loop:
+            cpu = cpu_baseline_pairs(seq, P, ns, args.method, cpu_threads)
+        else:
+            cpu = cpu_baseline(seq, ns, args.method, cpu_threads)
+    ms_step = dt / args.steps * 1e3
+    return {
+        "metric": ("ICP keyframe-pair registrations/sec (256k-ray Ouster-128, multi-scale)"
+                   if ouster else "ICP keyframe-pair registrations/sec (64k-pt scans)"),
+        "value": round(world * P * args.steps / dt, 3),
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32+f64",
+        "data": "synthetic (seeded ray-cast %s scans of a procedural scene)"
+                % ("Ouster-128" if ouster else "HDL-64"),
+        "config": ({"workload": f"ouster128_256k_{args.method}_multiscale_seq",
+                    "baseline_config": "BASELINE.json configs[4] (C5)",
+                    "pairs_per_gpu": P, "global_pairs": world * P,
+                    "points_per_scan_finest_voxel": int(np.mean(n_pts)),
+                    "rays_per_scan": 262144, "method": args.method,
+                    "voxel_scales": [0.4, 0.2, 0.1],
+                    "max_correspondence_distance": [2.0, 1.0, 0.5],
+                    "normals": f"hybrid r=0.3 max_nn=300, {normals}",
+                    "parallelism": f"dp{world}"}
+                   if ouster else
+                   {"workload": f"hdl64_64k_{args.method}_loop_closure_pairs",
+                    "baseline_config": "BASELINE.json configs[3] (C4: 4096 pairs over 8 GPUs)",
+                    "pairs_per_gpu": P, "global_pairs": world * P,
+                    "points_per_scan_post_filter": int(np.mean(n_pts)),
+                    "rays_per_scan": 65536, "method": args.method,
+                    "init": "GT (+) N(0.3 m, 3 deg yaw)",
+                    "max_correspondence_distance": 10.0,
+                    "normals": f"hybrid r=0.3 max_nn=300, {normals}",
+                    "parallelism": f"dp{world}"}
+                   if loop else
+                   {"workload": f"hdl64_64k_{args.method}_seq",
+                    "baseline_config": "BASELINE.json configs[2] (C3)",
+                    "pairs_per_gpu": P, "global_pairs": world * P,
+                    "streams_per_gpu": S,
+                    "points_per_scan_post_filter": int(np.mean(n_pts)),
+                    "rays_per_scan": 65536, "method": args.method,
+                    "max_correspondence_distance": 10.0,
+                    "normals": f"hybrid r=0.3 max_nn=300, {normals}",
+                    "parallelism": f"dp{world}"}),
+        "roofline": roof,
+        "roofline_normals": roof_n,
+        "cpu_baseline": cpu,
+        "mean_icp_iterations": float(np.mean(iters)),
+        "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
+                                  for k, v in stats.items() if v["launches"]},
+        "nn_uncertified_fraction_after_pass0": round(
+            cnt["nn_uncertified"] /
+            max(cnt["nn_queries"] - cnt["nn_queries_first_pass"], 1), 5),
+        "nn_fallback_fraction": {
+            "all_passes": round(cnt["nn_pending"] / max(cnt["nn_queries"], 1), 5),
+            "first_pass": round(cnt["nn_pending_first_pass"] /
+                                max(cnt["nn_queries_first_pass"], 1), 5)},
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from lidar_slam_arvc_amd import synthetic
+
+    W = args.workload
+    P0, seed0, _, normals0 = WORKLOAD_DEFAULTS[W]
+    normals = normals0 if args.normals == "auto" else args.normals
+    P = args.pairs_per_gpu or P0
+    seed = args.seed if args.seed >= 0 else seed0
+    # synthetic scans first, in forked worker processes: nothing in this process has touched the
+    # GPU yet (a fork after HIP initialisation is not safe)
+    procs = max(1, min(8, os.cpu_count() or 1))
+    seq = make_data(W, P, seed, rank * P, procs, args.seq_cache)
+    # the C4 / C5 blocks of the default line: each rank's own 512 pairs of BASELINE.json
+    # configs[3] / [4], the same bench step as --workload loop_closure / ouster_multiscale
+    extra = [] if args.no_c45 else [w for w in ("loop_closure", "ouster_multiscale") if w != W]
+    extra_seq = {w: make_data(w, WORKLOAD_DEFAULTS[w][0], WORKLOAD_DEFAULTS[w][1],
+                              rank * WORKLOAD_DEFAULTS[w][0], procs) for w in extra}
+    c1 = c2 = None
+    do_cpu = world == 1 and not args.no_cpu_baseline
+    if do_cpu and not args.no_c1:
+        # C1: 8k-point (16 x 512 ray) P2P pairs, seed 1 -- the reference's CPU-runnable case
+        c1 = synthetic.make_sequence(C1_PAIRS + 1, seed=1, model=synthetic.VLP16_8K,
+                                     processes=procs)
+        # C2: one 64k HDL-64 pair, seed 2
+        c2 = synthetic.make_sequence(2, seed=2, model=synthetic.HDL64, processes=procs)
+    cpu_threads = args.cpu_threads or usable_cores()
+    # the kernel hashes spawn llvm-objdump: before this process touches the GPU (every rank: the
+    # normals' PMC lookup runs on all of them)
+    for kernels in PMC_KERNELS.values():
+        kernel_sha(tuple(kernels))
+    _GPU_STARTED[0] = True
+
+    import torch
+    import torch.distributed as dist
+
+    # --share-gpu (a rehearsal of the N-rank path on a one-GPU box): every rank on device 0,
+    # collectives over gloo on host tensors; otherwise one GPU per rank and RCCL over xGMI
+    gpu = 0 if args.share_gpu else local
+    torch.cuda.set_device(gpu)
+    group = None
+    if world > 1:
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group = dist.group.WORLD
+    cuda = torch.device("cpu") if args.share_gpu else torch.device("cuda", local)   # collectives
+    common = dict(gpu=gpu, local=local, rank=rank, world=world, group=group, cuda=cuda,
+                  cpu_threads=cpu_threads)
+    grid_cells = ([float(c) for c in args.grid_cell_scales.split(",")]
+                  if args.grid_cell_scales else None)
+    out = run_workload(W, seq, P, args, normals=normals, streams=args.streams,
+                       grid_cell=args.grid_cell, grid_cells=grid_cells, do_cpu=do_cpu,
+                       cpu_sample=args.cpu_sample_pairs, **common)
+    del seq
+    blocks = {}
+    for w in extra:
+        blocks[{"loop_closure": "c4", "ouster_multiscale": "c5"}[w]] = run_workload(
+            w, extra_seq.pop(w), WORKLOAD_DEFAULTS[w][0], args, normals=WORKLOAD_DEFAULTS[w][3],
+            do_cpu=do_cpu, **common)
     if rank == 0:
-        achieved = nn["algo_bytes"] / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0
-        # PMC traffic of the same workload (profiles/nn_traffic.json, tools/pmc_nn.sh)
-        tj, t_why = pmc_entry("nn_traffic.json", args.workload, P)
-        traffic = tj.get("hbm_bytes_per_launch") if tj else None
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "traffic_source": "profiles/nn_traffic.json" if tj else t_why,
-                "kernel": "correspondence pass: nn_kernel (stability check + box search) + "
-                          "nn_fallback",
-                "algo_bytes_per_launch": nn["algo_bytes"] / max(nn["launches"], 1),
-                "avg_launch_ms": nn["ms"] / max(nn["launches"], 1),
-                "launches": nn["launches"],
-                "per_kernel_ms_per_pass": {k: round(stats[k]["ms"] / max(nn["launches"], 1), 5)
-                                           for k in ("nn", "nn_fallback")}}
-        cpu = None
-        if do_cpu:
-            ns = args.cpu_sample_pairs or (32 if ouster else (72 if loop else 144))
-            ns = max(1, min(ns, P))
-            if ouster:
-                cpu = cpu_baseline_multiscale(seq, ns, args.method, cpu_threads)
-            elif loop:
-                cpu = cpu_baseline_pairs(seq, P, ns, args.method, cpu_threads)
-            else:
-                cpu = cpu_baseline(seq, ns, args.method, cpu_threads)
+        from lidar_slam_arvc_amd import _lib
+        dev = _lib.device(gpu)
         c1_out = c1_line(dev, c1, cpu_threads) if c1 is not None else None
         c2_out = c2_line(dev, c2, cpu_threads) if c2 is not None else None
-        ms_step = dt / args.steps * 1e3
-        out = {
-            "metric": ("ICP keyframe-pair registrations/sec (256k-ray Ouster-128, multi-scale)"
-                       if ouster else "ICP keyframe-pair registrations/sec (64k-pt scans)"),
-            "value": round(world * P * args.steps / dt, 3),
-            "unit": "pairs/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32+f64",
-            "data": "synthetic (seeded ray-cast %s scans of a procedural scene)"
-                    % ("Ouster-128" if ouster else "HDL-64"),
-            "config": ({"workload": f"ouster128_256k_{args.method}_multiscale_seq",
-                        "pairs_per_gpu": P, "global_pairs": world * P,
-                        "points_per_scan_finest_voxel": int(np.mean(n_pts)),
-                        "rays_per_scan": 262144, "method": args.method,
-                        "voxel_scales": [0.4, 0.2, 0.1],
-                        "max_correspondence_distance": [2.0, 1.0, 0.5],
-                        "normals": f"hybrid r=0.3 max_nn=300, {args.normals}", "parallelism": f"dp{world}"}
-                       if ouster else
-                       {"workload": f"hdl64_64k_{args.method}_loop_closure_pairs",
-                        "pairs_per_gpu": P, "global_pairs": world * P,
-                        "points_per_scan_post_filter": int(np.mean(n_pts)),
-                        "rays_per_scan": 65536, "method": args.method,
-                        "init": "GT (+) N(0.3 m, 3 deg yaw)",
-                        "max_correspondence_distance": 10.0,
-                        "normals": f"hybrid r=0.3 max_nn=300, {args.normals}", "parallelism": f"dp{world}"}
-                       if loop else
-                       {"workload": f"hdl64_64k_{args.method}_seq",
-                        "pairs_per_gpu": P, "global_pairs": world * P,
-                        "streams_per_gpu": max(1, min(args.streams, P)),
-                        "points_per_scan_post_filter": int(np.mean(n_pts)),
-                        "rays_per_scan": 65536, "method": args.method,
-                        "max_correspondence_distance": 10.0,
-                        "normals": f"hybrid r=0.3 max_nn=300, {args.normals}", "parallelism": f"dp{world}"}),
-            "roofline": roof,
-            "roofline_normals": roof_n,
-            "cpu_baseline": cpu,
-            "c1": c1_out,
-            "c2": c2_out,
-            "mean_icp_iterations": float(np.mean(iters)),
-            "library_sources_sha256": source_sha(),
-            "breakdown_ms_per_step": {k: round(v["ms"] / args.steps, 3)
-                                      for k, v in stats.items() if v["launches"]},
-            "nn_uncertified_fraction_after_pass0": round(
-                cnt["nn_uncertified"] /
-                max(cnt["nn_queries"] - cnt["nn_queries_first_pass"], 1), 5),
-            "nn_fallback_fraction": {
-                "all_passes": round(cnt["nn_pending"] / max(cnt["nn_queries"], 1), 5),
-                "first_pass": round(cnt["nn_pending_first_pass"] /
-                                    max(cnt["nn_queries_first_pass"], 1), 5)}
-        }
-        print(json.dumps(out), flush=True)
+        line = {k: v for k, v in out.items() if k not in ("mean_icp_iterations",
+                                                         "breakdown_ms_per_step",
+                                                         "nn_uncertified_fraction_after_pass0",
+                                                         "nn_fallback_fraction")}
+        line.update({"c1": c1_out, "c2": c2_out, **blocks,
+                     "mean_icp_iterations": out["mean_icp_iterations"],
+                     "library_sources_sha256": source_sha(),
+                     "breakdown_ms_per_step": out["breakdown_ms_per_step"],
+                     "nn_uncertified_fraction_after_pass0":
+                         out["nn_uncertified_fraction_after_pass0"],
+                     "nn_fallback_fraction": out["nn_fallback_fraction"]})
+        print(json.dumps(line), flush=True)
     if group is not None:
         dist.barrier()
         dist.destroy_process_group()
-    if ms is not None:
-        ms.release()
-    for i in ids:
-        dev.release(i)
-    for d, h in extra_ids:
-        d.release(h)
 
 
 if __name__ == "__main__":

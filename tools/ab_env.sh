@@ -5,7 +5,7 @@
 # bench args via BENCH_ARGS
 set -u
 OUT=gpurun_out/$1; shift; mkdir -p $OUT; export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:-"--no-cpu-baseline --no-c1 --seq-cache /tmp/lsm_hdl64_seq.npz --steps 3 --warmup 1"}
+ARGS=${BENCH_ARGS:-"--no-cpu-baseline --no-c1 --no-c45 --seq-cache /tmp/lsm_hdl64_seq.npz --steps 3 --warmup 1"}
 summ() { tail -1 "$1" | python3 -c "import json,sys; j=json.loads(sys.stdin.read()); b=j['breakdown_ms_per_step']; print('$2', j['value'], j['ms_per_step'], {k: b[k] for k in b if k in ('normals','nn','nn_fallback','accumulate','grid','normals_lazy')})"; }
 for spec in "$@"; do
   IFS=: read -r tag lib envs <<< "$spec"

@@ -9,6 +9,6 @@ if [ -n "$K" ]; then
   rc=$?; tail -2 $OUT/pytest_sel.log; grep -E "FAILED|ERROR" $OUT/pytest_sel.log | head; [ $rc -gt 1 ] && exit $rc
 fi
 for W in $WS; do
-  timeout -k 10 600 python bench.py --workload $W --no-cpu-baseline --seq-cache /tmp/lsm_$W.npz > $OUT/bench_$W.log 2>&1 || { tail -20 $OUT/bench_$W.log; exit 1; }
+  timeout -k 10 600 python bench.py --workload $W --no-cpu-baseline --no-c45 --seq-cache /tmp/lsm_$W.npz > $OUT/bench_$W.log 2>&1 || { tail -20 $OUT/bench_$W.log; exit 1; }
   tail -1 $OUT/bench_$W.log | python3 -c "import json,sys; j=json.loads(sys.stdin.read()); print('$W', j['value'], j['ms_per_step'], j['breakdown_ms_per_step'])"
 done

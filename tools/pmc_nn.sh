@@ -8,7 +8,7 @@
 set -u
 W=${1:-hdl64_seq}; shift || true
 OUT=gpurun_out/pmc_nn_$W; mkdir -p $OUT; export TMPDIR=/tmp
-ARGS="--workload $W --steps 2 --warmup 1 --no-cpu-baseline --seq-cache /tmp/lsm_$W.npz $*"
+ARGS="--workload $W --steps 2 --warmup 1 --no-cpu-baseline --no-c45 --seq-cache /tmp/lsm_$W.npz $*"
 timeout -k 10 300 python bench.py $ARGS > $OUT/plain.log 2>&1 || { echo "plain run failed"; tail -5 $OUT/plain.log; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex "nn_kernel|nn_fallback" \
