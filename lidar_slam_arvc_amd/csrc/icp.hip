@@ -918,6 +918,259 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
 }
 
 // ------------------------------------------------------------------------------------------
+// LDS-staged tile search (the passes that search every query: 0 and 1)
+// ------------------------------------------------------------------------------------------
+// A workgroup's 256 queries are consecutive points of the cell-sorted source, so they occupy a
+// few cells. The workgroup stages every target point of the cells within NN_TMARGIN cells of its
+// queries' cells into LDS -- one x-sorted run per (y, z) row of the box: a row's block parts
+// follow each other in x, and their global indices increase with x, so the row is one run in
+// (x, index) order -- and every lane then runs the box search of nn_query against the tile:
+// rows centre-out in z and y, pruned by their slab distance, an entry search and two walks per
+// row, all in LDS. Each staged point carries its global index (w bits), so the (d2, index) order
+// and every result are the global path's. A query is resolved when its best distance is below
+// the distance to every face of the staged box that is not the grid's boundary (the points
+// outside are farther); the rest continue with nn_query (warm-started from the tile's best) and
+// the fallback, so the results are bit-identical to nn_kernel<false> (test_search_path_variants).
+// A workgroup whose box holds more than NN_TCAP points (or rows / block parts than the tables
+// hold) searches as nn_kernel<false> does. CPU model of the tile sizes: tools/nn_tile_model.py.
+#ifndef LSM_NN_TCAP
+#define LSM_NN_TCAP 4096
+#endif
+constexpr int NN_TCAP = LSM_NN_TCAP;   // staged points (16 B each)
+constexpr int NN_TPARTS = 384;         // staged block parts (a row spans one part per 4 cells)
+constexpr int NN_TMARGIN = 1;          // cells staged around the queries' cells
+
+// one x-sorted LDS run [a, b) of a row at slab distance dyz2 (squared): entry search at qx, then
+// rightwards and leftwards while dx^2 + dyz2 <= the pruning radius (nn_query's scan_run on LDS)
+__device__ __forceinline__ void tile_run(const float4 *T, uint32_t a, uint32_t b, float qx,
+                                         float qy, float qz, float dyz2, Top3 &t2) {
+    uint32_t lo = a, hi = b;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (T[mid].x < qx) lo = mid + 1;
+        else hi = mid;
+    }
+    for (uint32_t k = lo; k < b; ++k) {
+        const float4 t = T[k];
+        const float dx = t.x - qx;
+        if (dx * dx + dyz2 > t2.lim) break;
+        top_add(sqd(t, qx, qy, qz), __float_as_int(t.w), t2);
+    }
+    for (int k = int(lo) - 1; k >= int(a); --k) {
+        const float4 t = T[k];
+        const float dx = qx - t.x;
+        if (dx * dx + dyz2 > t2.lim) break;
+        top_add(sqd(t, qx, qy, qz), __float_as_int(t.w), t2);
+    }
+}
+
+__device__ __forceinline__ int wg_reduce_min(int v, int *red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, LSM_WAVE));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    v = red[0];
+#pragma unroll
+    for (int q = 1; q < NN_THREADS / LSM_WAVE; ++q) v = min(v, red[q]);
+    __syncthreads();
+    return v;
+}
+
+__global__ void __launch_bounds__(NN_THREADS)
+nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
+               NNParams prm, int pass, int32_t *__restrict__ corr, int2 *__restrict__ rec,
+               FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n,
+               uint32_t queue_cap) {
+    __shared__ float4 tile[NN_TCAP];
+    __shared__ uint32_t p_a[NN_TPARTS];        // a block part's first global index
+    __shared__ uint32_t p_off[NN_TPARTS + 1];  // its first tile slot (exclusive scan)
+    __shared__ int red[NN_THREADS / LSM_WAVE];
+    BlockTask task;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && int64_t(gridDim.x) < int64_t(tp.plan[1]) * NXCD)
+        atomicOr(tp.err, 1);
+    if (plan_task(tp, st, blockIdx.x, task) <= 0) return;   // uniform per workgroup
+    const PairState &P = st[task.pair];
+    if (!P.active) return;
+    const CloudDev S = cds[P.src];
+    const CloudDev G = cds[P.tgt];
+    const int i = task.start + threadIdx.x;
+    const bool live = i < S.n;
+    const int64_t g = P.src_off + i;
+    float m = prm.m0;
+    if (live && P.iter > 0) m = motion_margin(P, lsm_ld(S.xyz, i), prm);
+    // the query point and its cell (clamped to the grid, as nn_query)
+    float qx = 0.f, qy = 0.f, qz = 0.f;
+    int cx = 0, cy = 0, cz = 0;
+    if (live) {
+        double x, y, z;
+        transform_point(P.T, lsm_ld(S.xyz, i), x, y, z);
+        qx = float(x);
+        qy = float(y);
+        qz = float(z);
+    }
+    const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
+                fz = (qz - G.oz) * G.inv_cell;
+    auto clampc = [](float f, int n) { return (int)fminf(fmaxf(floorf(f), 0.f), float(n - 1)); };
+    if (live && G.n > 0) {
+        cx = clampc(fx, G.nx);
+        cy = clampc(fy, G.ny);
+        cz = clampc(fz, G.nz);
+    }
+    const bool lq = live && G.n > 0;
+    // the staged box: the queries' cells +- NN_TMARGIN, clipped to the grid
+    const int x0 = max(wg_reduce_min(lq ? cx : INT_MAX, red) - NN_TMARGIN, 0);
+    const int x1 = min(-wg_reduce_min(lq ? -cx : INT_MAX, red) + NN_TMARGIN, G.nx - 1);
+    const int y0 = max(wg_reduce_min(lq ? cy : INT_MAX, red) - NN_TMARGIN, 0);
+    const int y1 = min(-wg_reduce_min(lq ? -cy : INT_MAX, red) + NN_TMARGIN, G.ny - 1);
+    const int z0 = max(wg_reduce_min(lq ? cz : INT_MAX, red) - NN_TMARGIN, 0);
+    const int z1 = min(-wg_reduce_min(lq ? -cz : INT_MAX, red) + NN_TMARGIN, G.nz - 1);
+    const bool boxed = G.n > 0 && x0 <= x1 && y0 <= y1 && z0 <= z1;   // some query is live
+    const int nyb = boxed ? y1 - y0 + 1 : 0, nzb = boxed ? z1 - z0 + 1 : 0;
+    const int np = boxed ? (x1 >> LSM_BLK_SHIFT) - (x0 >> LSM_BLK_SHIFT) + 1 : 0;  // parts per row
+    const int64_t nparts64 = int64_t(nyb) * nzb * np;
+    bool tiled = boxed && nparts64 <= NN_TPARTS;
+    int nparts = tiled ? int(nparts64) : 0;
+    if (tiled) {
+        // part bounds; each thread holds the lengths of two consecutive parts for the scan
+        uint32_t len[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int t = 2 * int(threadIdx.x) + h;
+            len[h] = 0;
+            if (t < nparts) {
+                const int r = t / np, j = t - r * np;
+                const int y = y0 + r % nyb, z = z0 + r / nyb;
+                const int xa = max(x0, ((x0 >> LSM_BLK_SHIFT) + j) << LSM_BLK_SHIFT);
+                const int xb = min(x1, xa | (LSM_BLK - 1));
+                const uint32_t a = lsm_ld(G.cell_start, lsm_cell_lin(G.nbx, G.nby, xa, y, z));
+                const uint32_t b = lsm_ld(G.cell_start, lsm_cell_lin(G.nbx, G.nby, xb, y, z) + 1);
+                p_a[t] = a;
+                len[h] = b - a;
+            }
+        }
+        // exclusive scan of the part lengths (2 per thread, in part order)
+        const uint32_t pair_sum = len[0] + len[1];
+        uint32_t x = pair_sum;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+        for (int off = 1; off < LSM_WAVE; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, LSM_WAVE);
+            if (lane >= off) x += y;
+        }
+        __shared__ uint32_t wsum[NN_THREADS / LSM_WAVE];
+        if (lane == LSM_WAVE - 1) wsum[w] = x;
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int q = 0; q < NN_THREADS / LSM_WAVE; ++q) {
+            before += q < w ? wsum[q] : 0;
+            total += wsum[q];
+        }
+        const uint32_t ex = before + x - pair_sum;
+        if (2 * int(threadIdx.x) < nparts) p_off[2 * threadIdx.x] = ex;
+        if (2 * int(threadIdx.x) + 1 < nparts) p_off[2 * threadIdx.x + 1] = ex + len[0];
+        if (threadIdx.x == 0) p_off[nparts] = total;
+        tiled = total <= uint32_t(NN_TCAP);
+        __syncthreads();
+        if (tiled) {
+            // copy: slot s -> its part (binary search over p_off) -> global index; four slots
+            // per round, their loads issued together
+            for (uint32_t s0 = threadIdx.x; s0 < total; s0 += 4 * NN_THREADS) {
+                uint32_t k[4];
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t s = s0 + uint32_t(u) * NN_THREADS;
+                    k[u] = 0xffffffffu;
+                    if (s < total) {
+                        int lo = 0, hi = nparts;   // the last part with p_off <= s
+                        while (hi - lo > 1) {
+                            const int mid = (lo + hi) >> 1;
+                            if (p_off[mid] <= s) lo = mid;
+                            else hi = mid;
+                        }
+                        k[u] = p_a[lo] + (s - p_off[lo]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k[u] != 0xffffffffu) v[u] = lsm_ld(G.xyz, k[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k[u] != 0xffffffffu)
+                        tile[s0 + uint32_t(u) * NN_THREADS] =
+                            make_float4(v[u].x, v[u].y, v[u].z, __int_as_float(int(k[u])));
+            }
+        }
+        __syncthreads();
+    }
+    int result = -1, a2 = -1;
+    float r = 0.f;
+    Top3 t2 = top3_init(-1, INFINITY, m);
+    bool pending = false;
+    if (live && tiled) {
+        const int prev = corr[g];
+        if (prev >= 0 && prev < G.n) t2 = top3_init(prev, sqd(lsm_ld(G.xyz, prev), qx, qy, qz), m);
+        const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
+        const int mz = max(cz - z0, z1 - cz), my = max(cy - y0, y1 - cy);
+#pragma unroll 1
+        for (int iz = 0; iz <= 2 * mz; ++iz) {
+            const int adz = (iz + 1) >> 1;
+            if (adz >= 2 && float((adz - 1) * (adz - 1)) * c2 >= t2.lim) break;
+            const int z = cz + ((iz & 1) ? -adz : adz);
+            if (z < z0 || z > z1) continue;
+            const float wz = slab_cells2(fz, z) * c2;
+            if (wz >= t2.lim) continue;
+#pragma unroll 1
+            for (int iy = 0; iy <= 2 * my; ++iy) {
+                const int ady = (iy + 1) >> 1;
+                if (ady >= 2 && wz + float((ady - 1) * (ady - 1)) * c2 >= t2.lim) break;
+                const int y = cy + ((iy & 1) ? -ady : ady);
+                if (y < y0 || y > y1) continue;
+                const float wyz = wz + slab_cells2(fy, y) * c2;
+                if (wyz >= t2.lim) continue;
+                const int row = (z - z0) * nyb + (y - y0);
+                const uint32_t a = p_off[row * np], b = p_off[(row + 1) * np];
+                if (b > a) tile_run(tile, a, b, qx, qy, qz, wyz, t2);
+            }
+        }
+        // every unstaged point is at least `bound` away (faces on the grid boundary bound nothing)
+        const float bx = fminf(x0 > 0 ? fx - float(x0) : INFINITY,
+                               x1 + 1 < G.nx ? float(x1 + 1) - fx : INFINITY);
+        const float by = fminf(y0 > 0 ? fy - float(y0) : INFINITY,
+                               y1 + 1 < G.ny ? float(y1 + 1) - fy : INFINITY);
+        const float bz = fminf(z0 > 0 ? fz - float(z0) : INFINITY,
+                               z1 + 1 < G.nz ? float(z1 + 1) - fz : INFINITY);
+        const float bound = fminf(bx, fminf(by, bz)) * G.cell;
+        const float bound2 = bound * bound * 0.99999f;
+        if (t2.bd2 <= bound2 || bound >= prm.maxc) {
+            if (t2.bidx >= 0 && t2.bd2 < prm.maxc2) {
+                result = t2.bidx;
+                a2 = t2.sidx;
+                r = rho_from(t2.lim, bound);
+            } else {
+                result = -1;
+                r = rho_from(t2.bd2, bound);
+            }
+        } else {
+            // not settled inside the tile: the global box search from the tile's best
+            float4 qp;
+            pending = !nn_query(P.T, S, G, i, t2.bidx, m, prm, result, a2, r, t2, qp, 0, 1,
+                                nullptr, P.iter >= prm.direct_iter);
+        }
+    } else if (live) {
+        float4 qp;
+        pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, 0, 1, nullptr,
+                            P.iter >= prm.direct_iter);
+    }
+    push_fallback(pending, task.pair, i, m, t2, queue, queue_n, queue_cap);
+    if (live) {
+        corr[g] = pending ? -2 : result;
+        if (!pending) rec[g] = rec_pack(a2, pass, r);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // exact fallback: one wave per unresolved query, expanding boxes (shells)
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ float gap2(float q, float lo, float hi) {
@@ -1708,6 +1961,9 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     // follows the first update, which moves the scans by centimetres to decimetres -- beyond
     // nearly every certificate -- so the check would only add its loads before the search
     const int CERT_FROM = std::max(1, int(lsm_knob("LSM_NN_CERT_FROM", 2)));
+    // LSM_NN_TILE: the passes that search every query stage each workgroup's target cells in
+    // LDS (nn_tile_kernel); 0: nn_kernel<false> reads the target from global memory
+    const bool tile_search = lsm_knob("LSM_NN_TILE", 1) != 0.0;
     double ms0 = 0.0;
     for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
     unsigned long long *d_nst = nullptr;
@@ -1754,7 +2010,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             else
                 nn_kernel<true, true><<<grid, NN_THREADS, 0, st>>>(
                     tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
-        } else if (pass < CERT_FROM || nocert)
+        } else if ((pass < CERT_FROM || nocert) && tile_search)
+            nn_tile_kernel<<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_corr, d_rec,
+                                                        d_q, d_qn + pass, qcap);
+        else if (pass < CERT_FROM || nocert)
             nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_hist, d_corr,
                                                                 d_rec, d_q, d_qn + pass, qcap,
                                                                 d_sqn + pass);
