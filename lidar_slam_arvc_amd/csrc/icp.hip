@@ -964,16 +964,21 @@ __device__ __forceinline__ void tile_run(const float4 *T, uint32_t a, uint32_t b
     }
 }
 
-__device__ __forceinline__ int wg_reduce_min(int v, int *red) {
+// workgroup minima of six ints (one barrier pair)
+__device__ __forceinline__ void wg_min6(int (&v)[6], int (*red)[NN_THREADS / LSM_WAVE]) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, LSM_WAVE));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    v = red[0];
+    for (int c = 0; c < 6; ++c) {
 #pragma unroll
-    for (int q = 1; q < NN_THREADS / LSM_WAVE; ++q) v = min(v, red[q]);
+        for (int off = 32; off > 0; off >>= 1) v[c] = min(v[c], __shfl_xor(v[c], off, LSM_WAVE));
+        if ((threadIdx.x & 63) == 0) red[c][threadIdx.x >> 6] = v[c];
+    }
     __syncthreads();
-    return v;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        v[c] = red[c][0];
+#pragma unroll
+        for (int q = 1; q < NN_THREADS / LSM_WAVE; ++q) v[c] = min(v[c], red[c][q]);
+    }
 }
 
 __global__ void __launch_bounds__(NN_THREADS)
@@ -984,7 +989,7 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
     __shared__ float4 tile[NN_TCAP];
     __shared__ uint32_t p_a[NN_TPARTS];        // a block part's first global index
     __shared__ uint32_t p_off[NN_TPARTS + 1];  // its first tile slot (exclusive scan)
-    __shared__ int red[NN_THREADS / LSM_WAVE];
+    __shared__ int red[6][NN_THREADS / LSM_WAVE];
     BlockTask task;
     if (blockIdx.x == 0 && threadIdx.x == 0 && int64_t(gridDim.x) < int64_t(tp.plan[1]) * NXCD)
         atomicOr(tp.err, 1);
@@ -1018,12 +1023,12 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
     }
     const bool lq = live && G.n > 0;
     // the staged box: the queries' cells +- NN_TMARGIN, clipped to the grid
-    const int x0 = max(wg_reduce_min(lq ? cx : INT_MAX, red) - NN_TMARGIN, 0);
-    const int x1 = min(-wg_reduce_min(lq ? -cx : INT_MAX, red) + NN_TMARGIN, G.nx - 1);
-    const int y0 = max(wg_reduce_min(lq ? cy : INT_MAX, red) - NN_TMARGIN, 0);
-    const int y1 = min(-wg_reduce_min(lq ? -cy : INT_MAX, red) + NN_TMARGIN, G.ny - 1);
-    const int z0 = max(wg_reduce_min(lq ? cz : INT_MAX, red) - NN_TMARGIN, 0);
-    const int z1 = min(-wg_reduce_min(lq ? -cz : INT_MAX, red) + NN_TMARGIN, G.nz - 1);
+    int ext[6] = {lq ? cx : INT_MAX, lq ? -cx : INT_MAX, lq ? cy : INT_MAX,
+                  lq ? -cy : INT_MAX, lq ? cz : INT_MAX, lq ? -cz : INT_MAX};
+    wg_min6(ext, red);
+    const int x0 = max(ext[0] - NN_TMARGIN, 0), x1 = min(-ext[1] + NN_TMARGIN, G.nx - 1);
+    const int y0 = max(ext[2] - NN_TMARGIN, 0), y1 = min(-ext[3] + NN_TMARGIN, G.ny - 1);
+    const int z0 = max(ext[4] - NN_TMARGIN, 0), z1 = min(-ext[5] + NN_TMARGIN, G.nz - 1);
     const bool boxed = G.n > 0 && x0 <= x1 && y0 <= y1 && z0 <= z1;   // some query is live
     const int nyb = boxed ? y1 - y0 + 1 : 0, nzb = boxed ? z1 - z0 + 1 : 0;
     const int np = boxed ? (x1 >> LSM_BLK_SHIFT) - (x0 >> LSM_BLK_SHIFT) + 1 : 0;  // parts per row
