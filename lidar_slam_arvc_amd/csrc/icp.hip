@@ -27,6 +27,7 @@
 #include <cstring>
 #include <numeric>
 #include <unordered_map>
+#include <type_traits>
 #include <vector>
 
 #include "lsm_ctx.h"
@@ -537,6 +538,9 @@ __device__ __forceinline__ void group_top3(Top3 &t, int L) {
 // is the plain per-lane search; a workgroup with few uncertified queries splits each over
 // several lanes, so a long search chain (a far or ambiguous query of a pair that keeps
 // iterating) is not left to one lane. Every lane of the group returns the same values.
+// GBUF: read the target through a buffer descriptor (G must then be wave-uniform), else through
+// 64-bit global addresses (the box-queue kernel, whose waves may hold queries of several pairs)
+template <bool GBUF = bool(LSM_NN_BUF)>
 __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, const CloudDev &G,
                                          int i, int prev, float m, const NNParams &prm,
                                          int &result, int &alt, float &rho, Top3 &t2, float4 &qp,
@@ -597,11 +601,11 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     const int z0 = max(cz - K, 0), z1 = min(cz + K, G.nz - 1);
     const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
     const uint32_t *cs = G.cell_start;
-#if LSM_NN_BUF
-    const BufPts gp = cloud_buf_pts(G);
-#else
-    const GlobalPts gp{G.xyz};
-#endif
+    typedef typename std::conditional<GBUF, BufPts, GlobalPts>::type Rd;
+    const Rd gp = [&]() {
+        if constexpr (GBUF) return cloud_buf_pts(G);
+        else return GlobalPts{G.xyz};
+    }();
     const int W = 2 * K + 1;
     // Rows are visited centre-out (offsets 0, -1, 1, -2, 2, ...: |offset| never decreases) and
     // a row at offset d in z (or y) is at least (|d| - 1) cells from the query's slab. Once that
@@ -941,7 +945,8 @@ constexpr int NN_TPARTS = 384;         // staged block parts (a row spans one pa
 constexpr int NN_TMARGIN = 1;          // cells staged around the queries' cells
 
 // one x-sorted LDS run [a, b) of a row at slab distance dyz2 (squared): entry search at qx, then
-// rightwards and leftwards while dx^2 + dyz2 <= the pruning radius (nn_query's scan_run on LDS)
+// rightwards and leftwards while dx^2 + dyz2 <= the pruning radius (nn_query's scan_run on LDS;
+// each walk reads its next point before testing the current one)
 __device__ __forceinline__ void tile_run(const float4 *T, uint32_t a, uint32_t b, float qx,
                                          float qy, float qz, float dyz2, Top3 &t2) {
     uint32_t lo = a, hi = b;
@@ -950,17 +955,25 @@ __device__ __forceinline__ void tile_run(const float4 *T, uint32_t a, uint32_t b
         if (T[mid].x < qx) lo = mid + 1;
         else hi = mid;
     }
-    for (uint32_t k = lo; k < b; ++k) {
-        const float4 t = T[k];
-        const float dx = t.x - qx;
-        if (dx * dx + dyz2 > t2.lim) break;
-        top_add(sqd(t, qx, qy, qz), __float_as_int(t.w), t2);
+    if (lo < b) {
+        float4 nx = T[lo];
+        for (uint32_t k = lo; k < b; ++k) {
+            const float4 t = nx;
+            if (k + 1 < b) nx = T[k + 1];
+            const float dx = t.x - qx;
+            if (dx * dx + dyz2 > t2.lim) break;
+            top_add(sqd(t, qx, qy, qz), __float_as_int(t.w), t2);
+        }
     }
-    for (int k = int(lo) - 1; k >= int(a); --k) {
-        const float4 t = T[k];
-        const float dx = qx - t.x;
-        if (dx * dx + dyz2 > t2.lim) break;
-        top_add(sqd(t, qx, qy, qz), __float_as_int(t.w), t2);
+    if (lo > a) {
+        float4 nx = T[lo - 1];
+        for (int k = int(lo) - 1; k >= int(a); --k) {
+            const float4 t = nx;
+            if (k > int(a)) nx = T[k - 1];
+            const float dx = qx - t.x;
+            if (dx * dx + dyz2 > t2.lim) break;
+            top_add(sqd(t, qx, qy, qz), __float_as_int(t.w), t2);
+        }
     }
 }
 
@@ -984,8 +997,7 @@ __device__ __forceinline__ void wg_min6(int (&v)[6], int (*red)[NN_THREADS / LSM
 __global__ void __launch_bounds__(NN_THREADS)
 nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
                NNParams prm, int pass, int32_t *__restrict__ corr, int2 *__restrict__ rec,
-               FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n,
-               uint32_t queue_cap) {
+               FallbackItem *__restrict__ box, uint32_t *__restrict__ box_n, uint32_t box_cap) {
     __shared__ float4 tile[NN_TCAP];
     __shared__ uint32_t p_a[NN_TPARTS];        // a block part's first global index
     __shared__ uint32_t p_off[NN_TPARTS + 1];  // its first tile slot (exclusive scan)
@@ -1109,10 +1121,10 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
         }
         __syncthreads();
     }
-    int result = -1, a2 = -1;
+    int result = -1, a2 = -1, warm = -1;
     float r = 0.f;
     Top3 t2 = top3_init(-1, INFINITY, m);
-    bool pending = false;
+    bool boxq = false;
     if (live && tiled) {
         const int prev = corr[g];
         if (prev >= 0 && prev < G.n) t2 = top3_init(prev, sqd(lsm_ld(G.xyz, prev), qx, qy, qz), m);
@@ -1158,20 +1170,80 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
                 r = rho_from(t2.bd2, bound);
             }
         } else {
-            // not settled inside the tile: the global box search from the tile's best
-            float4 qp;
-            pending = !nn_query(P.T, S, G, i, t2.bidx, m, prm, result, a2, r, t2, qp, 0, 1,
-                                nullptr, P.iter >= prm.direct_iter);
+            boxq = true;   // not settled inside the tile: the global box search, warm from the
+            warm = t2.bidx;   // tile's best
         }
     } else if (live) {
-        float4 qp;
-        pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, 0, 1, nullptr,
-                            P.iter >= prm.direct_iter);
+        boxq = true;           // no tile: the global box search, warm from the previous pass
+        warm = corr[g];
     }
-    push_fallback(pending, task.pair, i, m, t2, queue, queue_n, queue_cap);
-    if (live) {
-        corr[g] = pending ? -2 : result;
-        if (!pending) rec[g] = rec_pack(a2, pass, r);
+    // the global box searches run in nn_box_kernel (full occupancy: this kernel holds a tile),
+    // compacted into a queue, warm-started as above
+    {
+        const uint64_t bm = __ballot(boxq);
+        if (bm) {
+            const int lane = threadIdx.x & 63;
+            const int leader = __ffsll((unsigned long long)bm) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(box_n, (uint32_t)__popcll(bm));
+            base = __shfl(base, leader, LSM_WAVE);
+            if (boxq) {
+                const uint32_t slot = base + __popcll(bm & ((uint64_t(1) << lane) - 1));
+                if (slot < box_cap) box[slot] = {task.pair, i, warm, 0.f, 0.f, m};
+            }
+        }
+    }
+    if (live && !boxq) {
+        corr[g] = result;
+        rec[g] = rec_pack(a2, pass, r);
+    }
+}
+
+// The box searches the tile kernel could not settle: one lane per queued query (nn_query with the
+// queued warm start; a wave takes its lanes' pairs one at a time), unresolved ones on to the
+// fallback. Grid-stride over the queue (its length is on the device).
+#ifndef LSM_NN_BOX_WPE
+#define LSM_NN_BOX_WPE 6
+#endif
+__global__ void __launch_bounds__(NN_THREADS) __attribute__((amdgpu_waves_per_eu(LSM_NN_BOX_WPE)))
+nn_box_kernel(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
+              int pass, int32_t *__restrict__ corr, int2 *__restrict__ rec,
+              const FallbackItem *__restrict__ box, const uint32_t *__restrict__ box_n,
+              uint32_t box_cap, FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n,
+              uint32_t queue_cap) {
+    const uint32_t n = min(*box_n, box_cap);
+    for (uint32_t base = blockIdx.x * NN_THREADS; base < n; base += gridDim.x * NN_THREADS) {
+        const uint32_t t = base + threadIdx.x;
+        const bool live = t < n;
+        FallbackItem it{0, 0, -1, 0.f, 0.f, 0.f};
+        if (live) it = box[t];
+        int result = -1, a2 = -1;
+        float r = 0.f;
+        Top3 t2 = top3_init(-1, INFINITY, it.margin);
+        bool pending = false;
+        int64_t g = 0;
+        // one pair at a time (the lanes of a wave usually hold one or two): its target is then
+        // wave-uniform and read through a buffer descriptor, as in nn_kernel
+        bool todo = live;
+        for (uint64_t bm = __ballot(todo); bm; bm = __ballot(todo)) {
+            const int lead = __ffsll((unsigned long long)bm) - 1;
+            const int pr = __builtin_amdgcn_readfirstlane(__shfl(it.pair, lead, LSM_WAVE));
+            if (todo && it.pair == pr) {
+                const PairState &P = st[pr];
+                const CloudDev S = cds[P.src];
+                const CloudDev G = cds[P.tgt];
+                g = P.src_off + it.i;
+                float4 qp;
+                pending = !nn_query(P.T, S, G, it.i, it.best, it.margin, prm, result, a2, r, t2,
+                                    qp, 0, 1, nullptr, P.iter >= prm.direct_iter);
+                todo = false;
+            }
+        }
+        push_fallback(pending, it.pair, it.i, it.margin, t2, queue, queue_n, queue_cap);
+        if (live) {
+            corr[g] = pending ? -2 : result;
+            if (!pending) rec[g] = rec_pack(a2, pass, r);
+        }
     }
 }
 
@@ -1867,9 +1939,11 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     }
     const uint32_t qcap = uint32_t(nsrc_tot);
     FallbackItem *d_q = (FallbackItem *)ctx->buf("i_queue", size_t(qcap) * sizeof(FallbackItem));
+    // the box-search queue of the tiled passes (nn_tile_kernel -> nn_box_kernel)
+    FallbackItem *d_bq = (FallbackItem *)ctx->buf("i_boxq", size_t(qcap) * sizeof(FallbackItem));
     double *d_part = (double *)ctx->buf("i_part", size_t(std::max(slot, 1)) * LSM_ACC * 8);
     const int ncnt = max_iter + 2;
-    uint32_t *d_counters = (uint32_t *)ctx->buf("i_counters", size_t(ncnt) * 3 * 4);
+    uint32_t *d_counters = (uint32_t *)ctx->buf("i_counters", size_t(ncnt) * 4 * 4);
     double *d_bytes = (double *)ctx->buf("i_bytes", size_t(ncnt) * 8);
     unsigned long long *d_srcn = (unsigned long long *)ctx->buf("i_srcn", size_t(ncnt) * 8);
     int32_t *d_pref = (int32_t *)ctx->buf("i_pref", size_t(npairs + 1) * 4);
@@ -1879,7 +1953,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
     int32_t *d_err = (int32_t *)ctx->buf("i_err", 4);
-    if (!d_corr || !d_rec || !d_q || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
+    if (!d_corr || !d_rec || !d_q || !d_bq || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
         !d_plan || !d_flags || !d_err || !d_coarse) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
@@ -1887,7 +1961,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     uint32_t *d_qn = d_counters;            // [ncnt] fallback queue sizes per pass
     uint32_t *d_active = d_counters + ncnt; // [ncnt] active pairs after each pass
     uint32_t *d_sqn = d_counters + 2 * ncnt; // [ncnt] uncertified queries per pass
-    LSM_HIP_TRY(ctx, hipMemsetAsync(d_counters, 0, size_t(ncnt) * 3 * 4, st));
+    uint32_t *d_bqn = d_counters + 3 * ncnt; // [ncnt] box-search queue sizes (tiled passes)
+    LSM_HIP_TRY(ctx, hipMemsetAsync(d_counters, 0, size_t(ncnt) * 4 * 4, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_err, 0, 4, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_bytes, 0, size_t(ncnt) * 8, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_srcn, 0, size_t(ncnt) * 8, st));
@@ -1959,6 +2034,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
     } ev_return{ctx, pass_ev, passes};
     const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
+    const int box_grid = std::max(1, ctx->num_cus * 8);   // nn_box_kernel: grid-stride
     constexpr int PASS_LAG = 2;   // passes queued ahead of the last one read back
     // LSM_NN_NOCERT=1: search every query in every pass (no stability certificate) -- the
     // tests' proof that certified passes return bit-identical correspondences
@@ -2015,10 +2091,13 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             else
                 nn_kernel<true, true><<<grid, NN_THREADS, 0, st>>>(
                     tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
-        } else if ((pass < CERT_FROM || nocert) && tile_search)
+        } else if ((pass < CERT_FROM || nocert) && tile_search) {
             nn_tile_kernel<<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_corr, d_rec,
-                                                        d_q, d_qn + pass, qcap);
-        else if (pass < CERT_FROM || nocert)
+                                                        d_bq, d_bqn + pass, qcap);
+            nn_box_kernel<<<box_grid, NN_THREADS, 0, st>>>(d_ps, d_cd, prm, pass, d_corr, d_rec,
+                                                           d_bq, d_bqn + pass, qcap, d_q,
+                                                           d_qn + pass, qcap);
+        } else if (pass < CERT_FROM || nocert)
             nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_hist, d_corr,
                                                                 d_rec, d_q, d_qn + pass, qcap,
                                                                 d_sqn + pass);
