@@ -812,7 +812,10 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
           NNParams prm, int pass, const double *__restrict__ hist, int32_t *__restrict__ corr,
           int2 *__restrict__ rec, FallbackItem *__restrict__ queue,
           uint32_t *__restrict__ queue_n, uint32_t queue_cap, uint32_t *__restrict__ searched,
-          unsigned long long *__restrict__ stats = nullptr) {
+          unsigned long long *__restrict__ stats = nullptr,
+          const uint8_t *__restrict__ tiled = nullptr) {
+    // after nn_tile_kernel (same grid and plan): only the workgroups it did not tile
+    if (tiled && tiled[blockIdx.x]) return;
     NNStat ls{};
     NNStat *ns = STATS ? &ls : nullptr;
     // one task per workgroup: the host sizes the grid from an earlier pass's plan, which only
@@ -948,7 +951,7 @@ constexpr int NN_TMARGIN = 1;          // cells staged around the queries' cells
 // rightwards and leftwards while dx^2 + dyz2 <= the pruning radius (nn_query's scan_run on LDS;
 // each walk reads its next point before testing the current one)
 __device__ __forceinline__ void tile_run(const float4 *T, uint32_t a, uint32_t b, float qx,
-                                         float qy, float qz, float dyz2, Top3 &t2) {
+                                         float qy, float qz, float dyz2, float cap2, Top3 &t2) {
     uint32_t lo = a, hi = b;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -961,7 +964,7 @@ __device__ __forceinline__ void tile_run(const float4 *T, uint32_t a, uint32_t b
             const float4 t = nx;
             if (k + 1 < b) nx = T[k + 1];
             const float dx = t.x - qx;
-            if (dx * dx + dyz2 > t2.lim) break;
+            if (dx * dx + dyz2 > fminf(t2.lim, cap2)) break;
             top_add(sqd(t, qx, qy, qz), __float_as_int(t.w), t2);
         }
     }
@@ -971,7 +974,7 @@ __device__ __forceinline__ void tile_run(const float4 *T, uint32_t a, uint32_t b
             const float4 t = nx;
             if (k > int(a)) nx = T[k - 1];
             const float dx = qx - t.x;
-            if (dx * dx + dyz2 > t2.lim) break;
+            if (dx * dx + dyz2 > fminf(t2.lim, cap2)) break;
             top_add(sqd(t, qx, qy, qz), __float_as_int(t.w), t2);
         }
     }
@@ -997,7 +1000,8 @@ __device__ __forceinline__ void wg_min6(int (&v)[6], int (*red)[NN_THREADS / LSM
 __global__ void __launch_bounds__(NN_THREADS)
 nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
                NNParams prm, int pass, int32_t *__restrict__ corr, int2 *__restrict__ rec,
-               FallbackItem *__restrict__ box, uint32_t *__restrict__ box_n, uint32_t box_cap) {
+               FallbackItem *__restrict__ box, uint32_t *__restrict__ box_n, uint32_t box_cap,
+               uint8_t *__restrict__ tiled_out) {
     __shared__ float4 tile[NN_TCAP];
     __shared__ uint32_t p_a[NN_TPARTS];        // a block part's first global index
     __shared__ uint32_t p_off[NN_TPARTS + 1];  // its first tile slot (exclusive scan)
@@ -1005,9 +1009,15 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
     BlockTask task;
     if (blockIdx.x == 0 && threadIdx.x == 0 && int64_t(gridDim.x) < int64_t(tp.plan[1]) * NXCD)
         atomicOr(tp.err, 1);
-    if (plan_task(tp, st, blockIdx.x, task) <= 0) return;   // uniform per workgroup
+    if (plan_task(tp, st, blockIdx.x, task) <= 0) {   // uniform per workgroup
+        if (threadIdx.x == 0) tiled_out[blockIdx.x] = 1;   // nothing for nn_kernel either
+        return;
+    }
     const PairState &P = st[task.pair];
-    if (!P.active) return;
+    if (!P.active) {
+        if (threadIdx.x == 0) tiled_out[blockIdx.x] = 1;
+        return;
+    }
     const CloudDev S = cds[P.src];
     const CloudDev G = cds[P.tgt];
     const int i = task.start + threadIdx.x;
@@ -1046,7 +1056,12 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
     const int np = boxed ? (x1 >> LSM_BLK_SHIFT) - (x0 >> LSM_BLK_SHIFT) + 1 : 0;  // parts per row
     const int64_t nparts64 = int64_t(nyb) * nzb * np;
     bool tiled = boxed && nparts64 <= NN_TPARTS;
-    int nparts = tiled ? int(nparts64) : 0;
+    if (!tiled) {   // no query, or too many rows: nn_kernel searches this workgroup
+        if (threadIdx.x == 0) tiled_out[blockIdx.x] = boxed ? 0 : 1;
+        return;
+    }
+    if (threadIdx.x == 0) tiled_out[blockIdx.x] = 1;
+    int nparts = int(nparts64);
     if (tiled) {
         // part bounds; each thread holds the lengths of two consecutive parts for the scan
         uint32_t len[2];
@@ -1089,7 +1104,11 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
         if (threadIdx.x == 0) p_off[nparts] = total;
         tiled = total <= uint32_t(NN_TCAP);
         __syncthreads();
-        if (tiled) {
+        if (!tiled) {   // too many points: nn_kernel searches this workgroup from global memory
+            if (threadIdx.x == 0) tiled_out[blockIdx.x] = 0;
+            return;
+        }
+        {
             // copy: slot s -> its part (binary search over p_off) -> global index; four slots
             // per round, their loads issued together
             for (uint32_t s0 = threadIdx.x; s0 < total; s0 += 4 * NN_THREADS) {
@@ -1128,30 +1147,9 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
     if (live && tiled) {
         const int prev = corr[g];
         if (prev >= 0 && prev < G.n) t2 = top3_init(prev, sqd(lsm_ld(G.xyz, prev), qx, qy, qz), m);
-        const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
-        const int mz = max(cz - z0, z1 - cz), my = max(cy - y0, y1 - cy);
-#pragma unroll 1
-        for (int iz = 0; iz <= 2 * mz; ++iz) {
-            const int adz = (iz + 1) >> 1;
-            if (adz >= 2 && float((adz - 1) * (adz - 1)) * c2 >= t2.lim) break;
-            const int z = cz + ((iz & 1) ? -adz : adz);
-            if (z < z0 || z > z1) continue;
-            const float wz = slab_cells2(fz, z) * c2;
-            if (wz >= t2.lim) continue;
-#pragma unroll 1
-            for (int iy = 0; iy <= 2 * my; ++iy) {
-                const int ady = (iy + 1) >> 1;
-                if (ady >= 2 && wz + float((ady - 1) * (ady - 1)) * c2 >= t2.lim) break;
-                const int y = cy + ((iy & 1) ? -ady : ady);
-                if (y < y0 || y > y1) continue;
-                const float wyz = wz + slab_cells2(fy, y) * c2;
-                if (wyz >= t2.lim) continue;
-                const int row = (z - z0) * nyb + (y - y0);
-                const uint32_t a = p_off[row * np], b = p_off[(row + 1) * np];
-                if (b > a) tile_run(tile, a, b, qx, qy, qz, wyz, t2);
-            }
-        }
-        // every unstaged point is at least `bound` away (faces on the grid boundary bound nothing)
+        // every unstaged point is at least `bound` away (faces on the grid boundary bound
+        // nothing): the search only needs the points within it (a query with none there goes to
+        // the box queue), so its rows and walks are pruned at that radius as well
         const float bx = fminf(x0 > 0 ? fx - float(x0) : INFINITY,
                                x1 + 1 < G.nx ? float(x1 + 1) - fx : INFINITY);
         const float by = fminf(y0 > 0 ? fy - float(y0) : INFINITY,
@@ -1160,6 +1158,31 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
                                z1 + 1 < G.nz ? float(z1 + 1) - fz : INFINITY);
         const float bound = fminf(bx, fminf(by, bz)) * G.cell;
         const float bound2 = bound * bound * 0.99999f;
+        const float cap2 = bound * bound * 1.0001f + 1e-6f;   // >= bound2 (f32 slack)
+        const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
+        const int mz = max(cz - z0, z1 - cz), my = max(cy - y0, y1 - cy);
+#pragma unroll 1
+        for (int iz = 0; iz <= 2 * mz; ++iz) {
+            const int adz = (iz + 1) >> 1;
+            if (adz >= 2 && float((adz - 1) * (adz - 1)) * c2 >= fminf(t2.lim, cap2)) break;
+            const int z = cz + ((iz & 1) ? -adz : adz);
+            if (z < z0 || z > z1) continue;
+            const float wz = slab_cells2(fz, z) * c2;
+            if (wz >= fminf(t2.lim, cap2)) continue;
+#pragma unroll 1
+            for (int iy = 0; iy <= 2 * my; ++iy) {
+                const int ady = (iy + 1) >> 1;
+                if (ady >= 2 && wz + float((ady - 1) * (ady - 1)) * c2 >= fminf(t2.lim, cap2))
+                    break;
+                const int y = cy + ((iy & 1) ? -ady : ady);
+                if (y < y0 || y > y1) continue;
+                const float wyz = wz + slab_cells2(fy, y) * c2;
+                if (wyz >= fminf(t2.lim, cap2)) continue;
+                const int row = (z - z0) * nyb + (y - y0);
+                const uint32_t a = p_off[row * np], b = p_off[(row + 1) * np];
+                if (b > a) tile_run(tile, a, b, qx, qy, qz, wyz, cap2, t2);
+            }
+        }
         if (t2.bd2 <= bound2 || bound >= prm.maxc) {
             if (t2.bidx >= 0 && t2.bd2 < prm.maxc2) {
                 result = t2.bidx;
@@ -1173,9 +1196,6 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
             boxq = true;   // not settled inside the tile: the global box search, warm from the
             warm = t2.bidx;   // tile's best
         }
-    } else if (live) {
-        boxq = true;           // no tile: the global box search, warm from the previous pass
-        warm = corr[g];
     }
     // the global box searches run in nn_box_kernel (full occupancy: this kernel holds a tile),
     // compacted into a queue, warm-started as above
@@ -1941,6 +1961,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     FallbackItem *d_q = (FallbackItem *)ctx->buf("i_queue", size_t(qcap) * sizeof(FallbackItem));
     // the box-search queue of the tiled passes (nn_tile_kernel -> nn_box_kernel)
     FallbackItem *d_bq = (FallbackItem *)ctx->buf("i_boxq", size_t(qcap) * sizeof(FallbackItem));
+    uint8_t *d_tiled = nullptr;   // per grid slot: 1 = nn_tile_kernel settled the workgroup
     double *d_part = (double *)ctx->buf("i_part", size_t(std::max(slot, 1)) * LSM_ACC * 8);
     const int ncnt = max_iter + 2;
     uint32_t *d_counters = (uint32_t *)ctx->buf("i_counters", size_t(ncnt) * 4 * 4);
@@ -2013,6 +2034,11 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     for (int64_t k = 0; k < npairs; ++k) total_blk += ps[k].nblk;
     const int64_t per0 = (total_blk + NXCD - 1) / NXCD;
     int grid = int(std::max<int64_t>(per0 * NXCD, NXCD));
+    d_tiled = (uint8_t *)ctx->buf("i_tiled", size_t(grid));   // the grid only shrinks
+    if (!d_tiled) {
+        ctx->set_error("scratch allocation failed: i_tiled");
+        return LSM_ENOMEM;
+    }
     int32_t *h_poll = (int32_t *)ctx->host_pinned(size_t(ncnt) * 3 * 4);
     if (!h_poll) {
         ctx->set_error("pinned allocation failed (icp poll words)");
@@ -2093,7 +2119,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                     tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap, d_sqn + pass, sp);
         } else if ((pass < CERT_FROM || nocert) && tile_search) {
             nn_tile_kernel<<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_corr, d_rec,
-                                                        d_bq, d_bqn + pass, qcap);
+                                                        d_bq, d_bqn + pass, qcap, d_tiled);
+            nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_hist, d_corr,
+                                                          d_rec, d_q, d_qn + pass, qcap,
+                                                          d_sqn + pass, nullptr, d_tiled);
             nn_box_kernel<<<box_grid, NN_THREADS, 0, st>>>(d_ps, d_cd, prm, pass, d_corr, d_rec,
                                                            d_bq, d_bqn + pass, qcap, d_q,
                                                            d_qn + pass, qcap);

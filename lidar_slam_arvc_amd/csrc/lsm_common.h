@@ -32,6 +32,8 @@ struct CloudDev {
     int n;
     const uint32_t *perm;       // sorted position -> reference order
     const float4 *prior_ref;    // prior normals in reference order (orientation), or nullptr
+    const double *xyz64;        // f64 coordinates in reference order (a voxelised cloud's f64
+                                // centroids: what Open3D's cloud holds), or nullptr
 };
 
 #define LSM_XYZ_PAD 16     // spare float4 points allocated past every processed cloud's end

@@ -1413,13 +1413,45 @@ __device__ bool hybrid_lane(const CloudDev &C, int j, const NormalParams &np,
 // The normal of point j from its neighbourhood Kk[0 .. m) (LDS, stride STRIDE words) in
 // the search's order, in Open3D's arithmetic (ComputeCovariance: raw f64 cumulants in that
 // order, each divided by n; FastEigen3x3).
+// The f64 coordinates of sorted point k as Open3D's cloud holds them: a voxelised cloud's f64
+// centroid (C.xyz64, reference order), else the f32 point. The small neighbourhoods' covariance
+// is decided by rounding (rank-deficient), so it must see the same coordinates: at C5's 0.4 m
+// scale nearly every neighbourhood is small, and the f32 rounding of the centroids alone moved
+// 12 of 512 coarse-stage registrations past the bar (tools/bench_parity.py).
+__device__ __forceinline__ void pt_f64(const CloudDev &C, uint32_t k, double &x, double &y,
+                                       double &z) {
+    if (C.xyz64) {
+        const size_t r = size_t(lsm_ld(C.perm, k)) * 3;
+        x = lsm_ld(C.xyz64, r);
+        y = lsm_ld(C.xyz64, r + 1);
+        z = lsm_ld(C.xyz64, r + 2);
+    } else {
+        const float4 p = lsm_ld(C.xyz, k);
+        x = p.x;
+        y = p.y;
+        z = p.z;
+    }
+}
+
+// the exact squared distance that orders a small neighbourhood: nanoflann's ((dx^2 + dy^2) +
+// dz^2) of the f64 coordinates for a voxelised cloud, else the walks' exact d2 of the f32 points
+__device__ __forceinline__ double small_d2(const CloudDev &C, double qx, double qy, double qz,
+                                           uint32_t k) {
+    if (C.xyz64) {
+        double x, y, z;
+        pt_f64(C, k, x, y, z);
+        return lsm_sqdist64(qx, qy, qz, x, y, z);
+    }
+    return make_off(lsm_ld(C.xyz, k), qx, qy, qz).d2;
+}
+
 template <int STRIDE>
 __device__ __forceinline__ void small_cov_normal(const CloudDev &C, int j, const uint32_t *Kk,
                                                  int m) {
     double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0, c4 = 0.0, c5 = 0.0, c6 = 0.0, c7 = 0.0, c8 = 0.0;
     for (int q = 0; q < m; ++q) {
-        const float4 p = lsm_ld(C.xyz, Kk[q * STRIDE]);
-        const double x = p.x, y = p.y, z = p.z;
+        double x, y, z;
+        pt_f64(C, Kk[q * STRIDE], x, y, z);
         c0 = lsm_dadd(c0, x);
         c1 = lsm_dadd(c1, y);
         c2 = lsm_dadd(c2, z);
@@ -1459,7 +1491,7 @@ __device__ __forceinline__ bool small_before(const CloudDev &C, double qx, doubl
                                              uint32_t fk, double dk, uint32_t k, uint32_t fq,
                                              uint32_t kq) {
     if (fk != fq) return fk < fq;
-    const double dq = make_off(lsm_ld(C.xyz, kq), qx, qy, qz).d2;
+    const double dq = small_d2(C, qx, qy, qz, kq);
     return dk < dq || (dk == dq && lsm_ld(C.perm, k) < lsm_ld(C.perm, kq));
 }
 
@@ -1472,16 +1504,18 @@ __device__ __forceinline__ void small_normal(const CloudDev &C, int j, const Nor
     const int cap = np.max_nn < CAP ? np.max_nn : CAP;
     const float4 qf = lsm_ld(C.xyz, j);
     const double qx = qf.x, qy = qf.y, qz = qf.z;
+    double ox, oy, oz;   // the query as the ordering sees it (pt_f64)
+    pt_f64(C, uint32_t(j), ox, oy, oz);
     int m = 0;
     const NormalsPts pts = normals_pts(C);
     ball_visit_runs(C, qf, np.r, [&](uint32_t a, uint32_t b, float xl, float xh) {
         scan_run_pred<2, 1>(pts, a, b, xl, xh, [&](const float4 &p, uint32_t k, bool in) {
             Off o;
             if (!in || !in_ball(np, qf, qx, qy, qz, p, o)) return;
-            const uint32_t fk = __float_as_uint(float(o.d2));   // non-negative: orders as u32
+            const double dk = C.xyz64 ? small_d2(C, ox, oy, oz, k) : o.d2;
+            const uint32_t fk = __float_as_uint(float(dk));   // non-negative: orders as u32
             auto before = [&](int q) {
-                return small_before(C, qx, qy, qz, fk, o.d2, k, F[q * STRIDE],
-                                    Kk[q * STRIDE]);
+                return small_before(C, ox, oy, oz, fk, dk, k, F[q * STRIDE], Kk[q * STRIDE]);
             };
             int pos;
             if (m < cap) pos = m++;
@@ -1503,11 +1537,11 @@ __device__ __forceinline__ void small_normal(const CloudDev &C, int j, const Nor
 template <int STRIDE>
 __device__ __forceinline__ void small_normal_from_list(const CloudDev &C, int j, uint32_t *F,
                                                        uint32_t *Kk, int m) {
-    const float4 qf = lsm_ld(C.xyz, j);
-    const double qx = qf.x, qy = qf.y, qz = qf.z;
+    double qx, qy, qz;   // the query as the ordering sees it (pt_f64)
+    pt_f64(C, uint32_t(j), qx, qy, qz);
     for (int a = 0; a < m; ++a) {
         const uint32_t k = Kk[a * STRIDE];
-        const double dk = make_off(lsm_ld(C.xyz, k), qx, qy, qz).d2;
+        const double dk = small_d2(C, qx, qy, qz, k);
         const uint32_t fk = __float_as_uint(float(dk));
         int pos = a;
         for (; pos > 0 && small_before(C, qx, qy, qz, fk, dk, k, F[(pos - 1) * STRIDE],
@@ -2358,6 +2392,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         D.nbz = geo[k].nbz;
         D.n = int(wn[k]);
         D.perm = c->d_perm;
+        D.xyz64 = (vox && c->d_vox) ? c->d_vox : nullptr;   // the f64 centroids (reference order)
         D.prior_ref = (p.want_normals && c->d_prior_ref && c->prior_n == int64_t(wn[k]))
                           ? c->d_prior_ref : nullptr;
         perm_ptrs[k] = c->d_perm;
@@ -3028,6 +3063,7 @@ int lsm_voxel_normals_run(lsm_ctx *ctx, Cloud *c, double v, Cloud *o) {
     LSM_HIP_TRY(ctx, hipStreamSynchronize(st));
     LSM_HIP_TRY(ctx, hipGetLastError());
     o->dev.nrm = o->d_nrm;
+    o->dev.xyz64 = o->d_vox;   // normals estimated on it later see the f64 centroids
     o->has_normals = true;
     o->voxelized = true;
     return LSM_OK;
