@@ -940,6 +940,7 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
 // the fallback, so the results are bit-identical to nn_kernel<false> (test_search_path_variants).
 // A workgroup whose box holds more than NN_TCAP points (or rows / block parts than the tables
 // hold) searches as nn_kernel<false> does. CPU model of the tile sizes: tools/nn_tile_model.py.
+// Off by default (LSM_NN_TILE=1 selects it): exact, but slower than the global path.
 #ifndef LSM_NN_TCAP
 #define LSM_NN_TCAP 4096
 #endif
@@ -2068,9 +2069,11 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     // follows the first update, which moves the scans by centimetres to decimetres -- beyond
     // nearly every certificate -- so the check would only add its loads before the search
     const int CERT_FROM = std::max(1, int(lsm_knob("LSM_NN_CERT_FROM", 2)));
-    // LSM_NN_TILE: the passes that search every query stage each workgroup's target cells in
-    // LDS (nn_tile_kernel); 0: nn_kernel<false> reads the target from global memory
-    const bool tile_search = lsm_knob("LSM_NN_TILE", 1) != 0.0;
+    // LSM_NN_TILE=1: the passes that search every query stage each workgroup's target cells in
+    // LDS (nn_tile_kernel + nn_box_kernel); default 0: nn_kernel<false> reads the target from
+    // global memory. Measured slower (nn 72.9 ms per C3 step global, 82.2 / 93.1 /
+    // 119.8 with tiles of 2048 / 3072 / 4096 points): an option, proven exact by the tests.
+    const bool tile_search = lsm_knob("LSM_NN_TILE", 0) != 0.0;
     double ms0 = 0.0;
     for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
     unsigned long long *d_nst = nullptr;

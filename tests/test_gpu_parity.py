@@ -407,7 +407,7 @@ def test_certified_passes_bit_identical(dev, method, max_corr, monkeypatch):
 
 @pytest.mark.parametrize("env", [{}, {"LSM_NN_SPLIT_PLACE": "1"}, {"LSM_NN_SPLIT_PLACE": "2"},
                                  {"LSM_NN_SPLIT": "32"}, {"LSM_NN_SPLIT": "1"},
-                                 {"LSM_NN_TILE": "0"}])
+                                 {"LSM_NN_TILE": "1"}])
 def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monkeypatch):
     """The bench's own data (seed-3 HDL-64 sequence), 24 pairs: enough pairs that the later
     passes leave workgroups with few uncertified queries, whose box searches are split over
@@ -448,7 +448,7 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monk
                                  {"LSM_NN_KMAX": "2"}, {"LSM_NN_KCOLD": "6", "LSM_NN_KMAX": "3"},
                                  {"LSM_NN_SPLIT_PLACE": "1"}, {"LSM_NN_SPLIT_PLACE": "2"},
                                  {"LSM_NN_NOCERT": "1"}, {"LSM_NN_COLD_SEED": "0"},
-                                 {"LSM_NN_TILE": "0"}, {"LSM_NN_TILE": "0", "LSM_NN_NOCERT": "1"}])
+                                 {"LSM_NN_TILE": "1"}, {"LSM_NN_TILE": "1", "LSM_NN_NOCERT": "1"}])
 def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     """The exact 1-NN may be reached along different paths: the stability check from pass 1, 2
     or 4, queries with a
@@ -456,8 +456,8 @@ def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     after the first update, the default 3 cells after 12 updates, or never), cold-start boxes
     of 3^3 / 5^3 / 9^3 (default) / 13^3 cells, warm boxes capped at 2 / 3 / 4 (default) cells,
     split groups placed anywhere in the workgroup, cold searches seeded with a point of the
-    query's own cell (default) or not, the full passes' searches from LDS-staged target tiles
-    (nn_tile_kernel, default) or from global memory (LSM_NN_TILE=0). Every choice
+    query's own cell (default) or not, the full passes' searches from global memory (default) or
+    from LDS-staged target tiles (LSM_NN_TILE=1: nn_tile_kernel + nn_box_kernel). Every choice
     must give the same correspondences, so every result is bit-identical to the default's
     (C4-style revisit pairs: large initial errors, many fallback queries)."""
     ps = synthetic.make_revisit_pairs(6, seed=41, model=synthetic.HDL64)
