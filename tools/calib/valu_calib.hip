@@ -1,7 +1,8 @@
-// Calibration of the SQ instruction counters on gfx950: kernels with a known number of VALU
-// instructions per wave (f32 FMA chains, f64 FMA chains), run under rocprofv3 --pmc SQ_WAVES
-// SQ_INSTS_VALU ... The ratio SQ_INSTS_VALU / SQ_WAVES against the disassembly's count per wave
-// tells how the counter counts a wave64 instruction (bench.py's roofline_normals divides by it).
+// Calibration of the SQ instruction counters and of the VALU issue rate on gfx950.
+// (1) SQ_INSTS_VALU / SQ_WAVES against a known count per wave: compiler-scheduled FMA chains
+//     (fma32: the compiler packs pairs into v_pk_fma_f32; fma64: v_fma_f64).
+// (2) Issue rate: inline-asm blocks of 8 independent v_fma_f32 / v_fma_f64 / v_add_f64 /
+//     v_pk_fma_f32 per iteration, 8 waves per SIMD -- wave-instructions per second per type.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -10,7 +11,7 @@ constexpr int N = 4096;
 __global__ void __launch_bounds__(256) fma32(float *out, float a, float b) {
     float x = float(threadIdx.x), y = x + 1.f, z = x + 2.f, w = x + 3.f;
 #pragma unroll 64
-    for (int i = 0; i < N; ++i) {   // 4 independent chains: 4 v_fma_f32 per iteration
+    for (int i = 0; i < N; ++i) {
         x = fmaf(x, a, b);
         y = fmaf(y, a, b);
         z = fmaf(z, a, b);
@@ -31,31 +32,74 @@ __global__ void __launch_bounds__(256) fma64(double *out, double a, double b) {
     out[blockIdx.x * 256 + threadIdx.x] = x + y + z + w;
 }
 
+constexpr int M = 1024;   // iterations of 8 independent instructions
+
+#define ASM8_F32(OP)                                                                       \
+    asm volatile(OP " %0, %8, %9, %0\n\t" OP " %1, %8, %9, %1\n\t" OP " %2, %8, %9, %2\n\t" \
+                 OP " %3, %8, %9, %3\n\t" OP " %4, %8, %9, %4\n\t" OP " %5, %8, %9, %5\n\t" \
+                 OP " %6, %8, %9, %6\n\t" OP " %7, %8, %9, %7"                             \
+                 : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) \
+                 : "v"(a), "v"(b))
+
+__global__ void __launch_bounds__(256) issue_f32(float *out, float a, float b) {
+    float r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4, r5 = r0 + 5,
+          r6 = r0 + 6, r7 = r0 + 7;
+    for (int i = 0; i < M; ++i) ASM8_F32("v_fma_f32");
+    out[blockIdx.x * 256 + threadIdx.x] = r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7;
+}
+
+__global__ void __launch_bounds__(256) issue_f64(double *out, double a, double b) {
+    double r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4, r5 = r0 + 5,
+           r6 = r0 + 6, r7 = r0 + 7;
+    for (int i = 0; i < M; ++i) ASM8_F32("v_fma_f64");
+    out[blockIdx.x * 256 + threadIdx.x] = r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7;
+}
+
+__global__ void __launch_bounds__(256) issue_add64(double *out, double a, double b) {
+    double r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4, r5 = r0 + 5,
+           r6 = r0 + 6, r7 = r0 + 7;
+    for (int i = 0; i < M; ++i)
+        asm volatile("v_add_f64 %0, %8, %0\n\tv_add_f64 %1, %8, %1\n\tv_add_f64 %2, %8, %2\n\t"
+                     "v_add_f64 %3, %8, %3\n\tv_add_f64 %4, %8, %4\n\tv_add_f64 %5, %8, %5\n\t"
+                     "v_add_f64 %6, %8, %6\n\tv_add_f64 %7, %8, %7"
+                     : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6),
+                       "+v"(r7)
+                     : "v"(a));
+    (void)b;
+    out[blockIdx.x * 256 + threadIdx.x] = r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7;
+}
+
+template <typename K, typename T>
+float timed(K k, T *o, T a, T b, int blocks) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    k<<<blocks, 256>>>(o, a, b);   // warm
+    (void)hipEventRecord(e0);
+    k<<<blocks, 256>>>(o, a, b);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms;
+}
+
 int main() {
-    const int blocks = 1024;
+    const int blocks = 2048;   // 8192 waves: 8 per SIMD on 256 CUs
     float *o32;
     double *o64;
     if (hipMalloc(&o32, blocks * 256 * 4) != hipSuccess || hipMalloc(&o64, blocks * 256 * 8) != hipSuccess) return 1;
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    for (int rep = 0; rep < 2; ++rep) {
-        hipEventRecord(e0);
-        fma32<<<blocks, 256>>>(o32, 0.999f, 0.001f);
-        hipEventRecord(e1);
-        hipEventSynchronize(e1);
-        float ms32;
-        hipEventElapsedTime(&ms32, e0, e1);
-        hipEventRecord(e0);
-        fma64<<<blocks, 256>>>(o64, 0.999, 0.001);
-        hipEventRecord(e1);
-        hipEventSynchronize(e1);
-        float ms64;
-        hipEventElapsedTime(&ms64, e0, e1);
-        const double insts = double(blocks) * 4 * 4.0 * N;   // wave-instructions of the chains
-        printf("rep %d: f32 %.3f ms (%.1f G wave-FMA/s), f64 %.3f ms (%.1f G wave-FMA/s); waves %d, "
-               "chain FMAs per wave %d\n", rep, ms32, insts / ms32 / 1e6, ms64, insts / ms64 / 1e6,
-               blocks * 4, 4 * N);
-    }
+    const double waves = blocks * 4.0;
+    float ms = timed(fma32, o32, 0.999f, 0.001f, blocks);
+    printf("fma32 (compiler, v_pk_fma_f32): %.3f ms, %.1f G wave-instr/s\n", ms, waves * (N * 2.0) / ms / 1e6);
+    ms = timed(fma64, o64, 0.999, 0.001, blocks);
+    printf("fma64 (compiler, v_fma_f64): %.3f ms, %.1f G wave-instr/s\n", ms, waves * (N * 4.0) / ms / 1e6);
+    ms = timed(issue_f32, o32, 0.999f, 0.001f, blocks);
+    printf("issue v_fma_f32 x8: %.3f ms, %.1f G wave-instr/s\n", ms, waves * (M * 8.0) / ms / 1e6);
+    ms = timed(issue_f64, o64, 0.999, 0.001, blocks);
+    printf("issue v_fma_f64 x8: %.3f ms, %.1f G wave-instr/s\n", ms, waves * (M * 8.0) / ms / 1e6);
+    ms = timed(issue_add64, o64, 0.999, 0.001, blocks);
+    printf("issue v_add_f64 x8: %.3f ms, %.1f G wave-instr/s\n", ms, waves * (M * 8.0) / ms / 1e6);
+    printf("(peak assumed by bench.py: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles = 1228.8 G/s)\n");
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
