@@ -37,6 +37,10 @@ FP32_VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md chip-level parameters (vec
 # VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one 64-lane wave instruction per 2 cycles per
 # SIMD (MI355X_MICROARCH.md 'Wave scheduling'), in G wave-instructions/s
 VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 2   # = 1228.8
+# f64 add / fma wave-instructions issue at about half that: 498 (v_fma_f64) / 507 (v_add_f64) G/s
+# measured with 8 waves per SIMD and 8 independent chains (v_fma_f32 in the same kernel: 868 G/s;
+# tools/calib/valu_calib.hip, profiles/r05h/valu_calib.log)
+VALU_F64_PEAK_G = 500.0
 KERNELS = ["filter", "grid", "normals", "normals_lazy", "nn", "nn_fallback", "accumulate",
            "solve", "voxel"]
 
@@ -526,14 +530,20 @@ def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda
             npts = d0.kernel_stats("normals_points")["launches"]
             step_s = norm_ms / args.steps * 1e-3
             flops = 18.0 * nb + 150.0 * npts
-            valu, valu_k = None, None
+            valu, valu_k, f64 = None, None, None
             # PMC count of the same workload and normals mode (profiles/normals_valu.json)
             vj, v_why = pmc_entry("normals_valu.json", workload, P, normals)
             if vj:
                 valu = vj.get("valu_per_step")
-                valu_k = {k: v.get("SQ_INSTS_VALU")
-                          for k, v in vj.get("per_kernel_per_step", {}).items()}
+                pk = vj.get("per_kernel_per_step", {})
+                valu_k = {k: v.get("SQ_INSTS_VALU") for k, v in pk.items()}
+                f64 = sum(v.get("SQ_INSTS_VALU_ADD_F64", 0.0) + v.get("SQ_INSTS_VALU_FMA_F64", 0.0)
+                          for v in pk.values())
             ach = valu / step_s / 1e9 if valu else None
+            # issue time at peak with the f64 add / fma instructions at their measured rate (the
+            # other f64 instructions -- mul, conversions, compares -- are counted at the f32 rate)
+            t_peak = ((valu - f64) / (VALU_ISSUE_PEAK_G * 1e9) + f64 / (VALU_F64_PEAK_G * 1e9)
+                      if valu and f64 is not None else None)
             roof_n = {"bound": "valu", "kernel": "normals_sparse_kernel + normals_dense_kernel + "
                                                  "normals_refine_kernel (the split launch; " +
                                                  ("each keyframe's normals when it is first a "
@@ -546,6 +556,14 @@ def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda
                       "frac": round(ach / VALU_ISSUE_PEAK_G, 5) if ach else None,
                       "valu_instructions_per_step": valu,
                       "valu_instructions_per_kernel": valu_k,
+                      "f64_add_fma_per_step": f64,
+                      "f64_weighted": ({"issue_ms_at_peak": round(t_peak * 1e3, 3),
+                                        "frac": round(t_peak / step_s, 5),
+                                        "peaks_G_per_s": {"f64_add_fma": VALU_F64_PEAK_G,
+                                                          "other": VALU_ISSUE_PEAK_G},
+                                        "source": "tools/calib/valu_calib.hip "
+                                                  "(profiles/r05h/valu_calib.log)"}
+                                       if t_peak else None),
                       "ms_per_step": round(step_s * 1e3, 4),
                       "launches_per_step": (stats["normals"]["launches"] +
                                             stats["normals_lazy"]["launches"]) / args.steps,
