@@ -924,6 +924,46 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
     if (STATS) flush_stats(ls, stats);
 }
 
+// The passes that search every query (nn_kernel<false>'s work) with LQ lanes per query: the rows
+// of each query's box are dealt round-robin over its LQ lanes (nn_query's split search, merged by
+// group_top3), so a long search chain is shared; LQ * 256 threads per workgroup, one 256-query
+// block each. Exact like every split search (test_search_path_variants_bit_identical).
+template <int LQ>
+__global__ void __launch_bounds__(NN_THREADS * LQ) __attribute__((amdgpu_waves_per_eu(LSM_NN_WPE0)))
+nn_full_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
+               NNParams prm, int pass, int32_t *__restrict__ corr, int2 *__restrict__ rec,
+               FallbackItem *__restrict__ queue, uint32_t *__restrict__ queue_n,
+               uint32_t queue_cap) {
+    BlockTask task;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && int64_t(gridDim.x) < int64_t(tp.plan[1]) * NXCD)
+        atomicOr(tp.err, 1);
+    if (plan_task(tp, st, blockIdx.x, task) <= 0) return;
+    const PairState &P = st[task.pair];
+    if (!P.active) return;
+    const CloudDev S = cds[P.src];
+    const CloudDev G = cds[P.tgt];
+    const int sub = int(threadIdx.x) & (LQ - 1);
+    const int i = task.start + int(threadIdx.x) / LQ;
+    const bool live = i < S.n;
+    const int64_t g = P.src_off + i;
+    float m = prm.m0;
+    if (live && P.iter > 0) m = motion_margin(P, lsm_ld(S.xyz, i), prm);
+    int result = -1, a2 = -1;
+    float r = 0.f;
+    Top3 t2 = top3_init(-1, INFINITY, m);
+    bool pending = false;
+    float4 qp;
+    if (live)
+        pending = !nn_query(P.T, S, G, i, corr[g], m, prm, result, a2, r, t2, qp, sub, LQ,
+                            nullptr, P.iter >= prm.direct_iter);
+    const bool lead = live && sub == 0;
+    push_fallback(pending && lead, task.pair, i, m, t2, queue, queue_n, queue_cap);
+    if (lead) {
+        corr[g] = pending ? -2 : result;
+        if (!pending) rec[g] = rec_pack(a2, pass, r);
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // LDS-staged tile search (the passes that search every query: 0 and 1)
 // ------------------------------------------------------------------------------------------
@@ -2074,6 +2114,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     // global memory. Measured slower (nn 72.9 ms per C3 step global, 82.2 / 93.1 /
     // 119.8 with tiles of 2048 / 3072 / 4096 points): an option, proven exact by the tests.
     const bool tile_search = lsm_knob("LSM_NN_TILE", 0) != 0.0;
+    // LSM_NN_FULL_L: lanes per query in the passes that search every query (1, 2 or 4)
+    const int full_l = int(lsm_knob("LSM_NN_FULL_L", 1));
     double ms0 = 0.0;
     for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
     unsigned long long *d_nst = nullptr;
@@ -2129,7 +2171,13 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             nn_box_kernel<<<box_grid, NN_THREADS, 0, st>>>(d_ps, d_cd, prm, pass, d_corr, d_rec,
                                                            d_bq, d_bqn + pass, qcap, d_q,
                                                            d_qn + pass, qcap);
-        } else if (pass < CERT_FROM || nocert)
+        } else if ((pass < CERT_FROM || nocert) && full_l == 2)
+            nn_full_kernel<2><<<grid, NN_THREADS * 2, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_corr,
+                                                               d_rec, d_q, d_qn + pass, qcap);
+        else if ((pass < CERT_FROM || nocert) && full_l == 4)
+            nn_full_kernel<4><<<grid, NN_THREADS * 4, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_corr,
+                                                               d_rec, d_q, d_qn + pass, qcap);
+        else if (pass < CERT_FROM || nocert)
             nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_hist, d_corr,
                                                                 d_rec, d_q, d_qn + pass, qcap,
                                                                 d_sqn + pass);

@@ -448,7 +448,9 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monk
                                  {"LSM_NN_KMAX": "2"}, {"LSM_NN_KCOLD": "6", "LSM_NN_KMAX": "3"},
                                  {"LSM_NN_SPLIT_PLACE": "1"}, {"LSM_NN_SPLIT_PLACE": "2"},
                                  {"LSM_NN_NOCERT": "1"}, {"LSM_NN_COLD_SEED": "0"},
-                                 {"LSM_NN_TILE": "1"}, {"LSM_NN_TILE": "1", "LSM_NN_NOCERT": "1"}])
+                                 {"LSM_NN_TILE": "1"}, {"LSM_NN_TILE": "1", "LSM_NN_NOCERT": "1"},
+                                 {"LSM_NN_FULL_L": "2"}, {"LSM_NN_FULL_L": "4"},
+                                 {"LSM_NN_FULL_L": "2", "LSM_NN_NOCERT": "1"}])
 def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     """The exact 1-NN may be reached along different paths: the stability check from pass 1, 2
     or 4, queries with a
