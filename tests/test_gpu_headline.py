@@ -9,11 +9,10 @@ f64 restatements of Open3D's path, from committed fixtures:
   (tools/bench_parity.py --make-cpu); test_headline_full_sequence_vs_cpp_oracle runs the whole
   batch against it.
 
-Bars (north_star): |dR| <= 1e-4 per element and |dt| <= 1e-3 m on converged pairs. Where the
-two oracles themselves disagree beyond that bar the reference answer is not defined by the
-algorithm (normals of rank-deficient neighbourhoods -- e.g. three collinear points -- are
-decided by rounding; the oracles sum the raw cumulants in different orders, and so would two
-Open3D builds), and the pair must match at least one of them. Pairs that do not converge within
+Bars (north_star): |dR| <= 1e-4 per element and |dt| <= 1e-3 m on converged pairs, against
+both oracles: they agree on all 32 pairs (normals of rank-deficient neighbourhoods -- e.g. three
+collinear points -- are decided by rounding, and both oracles now use Open3D's raw cumulants
+divided by n for them), so no pair may lean on either one alone. Pairs that do not converge within
 30 updates are held to equal quality: fitness within 1e-3 and rmse no worse than 5 % above the
 oracle's (chaotic registrations).
 """
@@ -75,10 +74,10 @@ def test_headline_pairs_vs_both_oracles(headline):
         ok_py, ok_c = _within(Tg, Tp), _within(Tg, Tc)
         rows.append((int(k), conv, oracles_agree, ok_py, ok_c))
         if conv:
-            if oracles_agree:
-                assert ok_py, f"pair {k}: GPU outside the bar of the (well-defined) oracle"
-            else:
-                assert ok_py or ok_c, f"pair {k}: GPU matches neither oracle"
+            # the two oracles agree on every one of these pairs (since round 4's C++ oracle
+            # divides its cumulants as Open3D does), so the GPU must be within the bar of both
+            assert oracles_agree, f"pair {k}: the oracles disagree (fixture changed?)"
+            assert ok_py and ok_c, f"pair {k}: GPU outside the bar (NumPy {ok_py}, C++ {ok_c})"
         else:
             assert abs(got["fitness"][m] - py["fitness"][m]) < 1e-3, f"pair {k}"
             assert got["inlier_rmse"][m] < 1.05 * py["inlier_rmse"][m], f"pair {k}"
