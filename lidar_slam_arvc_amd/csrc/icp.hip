@@ -644,7 +644,7 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
             // 81.7 -> 91.3 ms per step, 88.5 with the registers capped back to 7 waves/SIMD.)
             int x = xa;
             while (x <= xb) {
-                const int xe = min(xb, x | (LSM_BLK - 1));   // end of this block's row part
+                const int xe = min(xb, x | (LSM_BLKX - 1));   // end of this block's row part
                 const uint32_t a = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, x, y, z));
                 const uint32_t b = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, xe, y, z) + 1);
                 if (b > a) scan_run(gp, a, b, qx, qy, qz, wyz, t2, prm.lin, ns);
@@ -1094,7 +1094,7 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
     const int z0 = max(ext[4] - NN_TMARGIN, 0), z1 = min(-ext[5] + NN_TMARGIN, G.nz - 1);
     const bool boxed = G.n > 0 && x0 <= x1 && y0 <= y1 && z0 <= z1;   // some query is live
     const int nyb = boxed ? y1 - y0 + 1 : 0, nzb = boxed ? z1 - z0 + 1 : 0;
-    const int np = boxed ? (x1 >> LSM_BLK_SHIFT) - (x0 >> LSM_BLK_SHIFT) + 1 : 0;  // parts per row
+    const int np = boxed ? (x1 >> LSM_BLKX_SHIFT) - (x0 >> LSM_BLKX_SHIFT) + 1 : 0;  // per row
     const int64_t nparts64 = int64_t(nyb) * nzb * np;
     bool tiled = boxed && nparts64 <= NN_TPARTS;
     if (!tiled) {   // no query, or too many rows: nn_kernel searches this workgroup
@@ -1113,8 +1113,8 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
             if (t < nparts) {
                 const int r = t / np, j = t - r * np;
                 const int y = y0 + r % nyb, z = z0 + r / nyb;
-                const int xa = max(x0, ((x0 >> LSM_BLK_SHIFT) + j) << LSM_BLK_SHIFT);
-                const int xb = min(x1, xa | (LSM_BLK - 1));
+                const int xa = max(x0, ((x0 >> LSM_BLKX_SHIFT) + j) << LSM_BLKX_SHIFT);
+                const int xb = min(x1, xa | (LSM_BLKX - 1));
                 const uint32_t a = lsm_ld(G.cell_start, lsm_cell_lin(G.nbx, G.nby, xa, y, z));
                 const uint32_t b = lsm_ld(G.cell_start, lsm_cell_lin(G.nbx, G.nby, xb, y, z) + 1);
                 p_a[t] = a;
@@ -1424,7 +1424,7 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
         transform_point(P.T, lsm_ld(S.xyz, q.i), qx64, qy64, qz64);
         const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
         Top2 t2 = top2_init(q.best, q.best_d2, q.second_d2, q.margin);
-        const float B = G.cell * float(LSM_BLK);
+        const float B = G.cell * float(LSM_BLK), Bx = G.cell * float(LSM_BLKX);   // block edges
         const float gx1 = G.ox + G.nx * G.cell, gy1 = G.oy + G.ny * G.cell,
                     gz1 = G.oz + G.nz * G.cell;
         const float box2 = gap2(qx, G.ox, gx1) + gap2(qy, G.oy, gy1) + gap2(qz, G.oz, gz1);
@@ -1435,8 +1435,8 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
             fbound = sqrtf(box2);
             if (sub == 0) fs[6] += 1;
         } else {
-            const float invB = 1.f / B;
-            const int qbx = (int)floorf((qx - G.ox) * invB), qby = (int)floorf((qy - G.oy) * invB),
+            const float invB = 1.f / B, invBx = 1.f / Bx;
+            const int qbx = (int)floorf((qx - G.ox) * invBx), qby = (int)floorf((qy - G.oy) * invB),
                       qbz = (int)floorf((qz - G.oz) * invB);
             auto outside = [](int v, int n) { return v < 0 ? -v : (v > n - 1 ? v - (n - 1) : 0); };
             const int r0 = max(outside(qbx, G.nbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
@@ -1465,7 +1465,7 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                         const int bx = qbx + dx, by = qby + dy, bz = qbz + dz;
                         if (bx >= 0 && bx < G.nbx && by >= 0 && by < G.nby && bz >= 0 &&
                             bz < G.nbz) {
-                            const float lb2 = gap2(qx, G.ox + bx * B, G.ox + (bx + 1) * B) +
+                            const float lb2 = gap2(qx, G.ox + bx * Bx, G.ox + (bx + 1) * Bx) +
                                               gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
                                               gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
                             if (lb2 * 0.9999f < t2.lim) {
@@ -1531,8 +1531,8 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                 group_top2<GL>(t2);
                 const int r = rb;
                 float bound = INFINITY;
-                if (qbx - r > 0) bound = fminf(bound, qx - (G.ox + (qbx - r) * B));
-                if (qbx + r + 1 < G.nbx) bound = fminf(bound, G.ox + (qbx + r + 1) * B - qx);
+                if (qbx - r > 0) bound = fminf(bound, qx - (G.ox + (qbx - r) * Bx));
+                if (qbx + r + 1 < G.nbx) bound = fminf(bound, G.ox + (qbx + r + 1) * Bx - qx);
                 if (qby - r > 0) bound = fminf(bound, qy - (G.oy + (qby - r) * B));
                 if (qby + r + 1 < G.nby) bound = fminf(bound, G.oy + (qby + r + 1) * B - qy);
                 if (qbz - r > 0) bound = fminf(bound, qz - (G.oz + (qbz - r) * B));

@@ -37,14 +37,23 @@ struct CloudDev {
 };
 
 #define LSM_XYZ_PAD 16     // spare float4 points allocated past every processed cloud's end
-#define LSM_BLK 4          // cells per block edge
+#define LSM_BLK 4          // cells per block edge in y and z
 #define LSM_BLK_SHIFT 2
-#define LSM_BLK_CELLS 64
+// cells per block edge in x: 1 << LSM_BLKX_SHIFT. A row of cells inside a block is one
+// contiguous, x-sorted run, so wider blocks cut the rows the walks visit into fewer runs.
+#ifndef LSM_BLKX_SHIFT
+#define LSM_BLKX_SHIFT 2
+#endif
+#define LSM_BLKX (1 << LSM_BLKX_SHIFT)
+#define LSM_BLK_CELLS (LSM_BLKX * LSM_BLK * LSM_BLK)
 
-// blocked linear cell index (see layout note above)
+// blocked linear cell index (see layout note above): blocks z-major, then cells z-major inside
+// a block, x fastest
 __host__ __device__ __forceinline__ int lsm_cell_lin(int nbx, int nby, int x, int y, int z) {
-    const int bx = x >> LSM_BLK_SHIFT, by = y >> LSM_BLK_SHIFT, bz = z >> LSM_BLK_SHIFT;
-    return (((bz * nby + by) * nbx + bx) << 6) | ((z & 3) << 4) | ((y & 3) << 2) | (x & 3);
+    const int bx = x >> LSM_BLKX_SHIFT, by = y >> LSM_BLK_SHIFT, bz = z >> LSM_BLK_SHIFT;
+    return (((bz * nby + by) * nbx + bx) << (LSM_BLKX_SHIFT + 2 * LSM_BLK_SHIFT)) |
+           ((z & (LSM_BLK - 1)) << (LSM_BLKX_SHIFT + LSM_BLK_SHIFT)) |
+           ((y & (LSM_BLK - 1)) << LSM_BLKX_SHIFT) | (x & (LSM_BLKX - 1));
 }
 
 // Per-pair ICP state (device). Layout kept 8-byte aligned.

@@ -465,7 +465,7 @@ struct GridGeo {
     uint32_t cell_off;     // offset of this cloud in the global cell space
     uint32_t pt_off;       // offset of this cloud in the batch point arrays
     uint32_t n;
-    uint32_t ncells;       // nbx * nby * nbz * 64 (blocked, padded)
+    uint32_t ncells;       // nbx * nby * nbz * LSM_BLK_CELLS (blocked, padded)
 };
 
 __device__ __forceinline__ int cell_coord(float v, float o, float inv, int nmax) {
@@ -789,7 +789,7 @@ __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, fl
             const float xl = qf.x - ch, xh = qf.x + ch;
             int x = xlo;
             while (x <= xhi) {
-                const int xe = min(xhi, x | (LSM_BLK - 1));   // end of this block's row part
+                const int xe = min(xhi, x | (LSM_BLKX - 1));   // end of this block's row part
                 const int l0 = lsm_cell_lin(C.nbx, C.nby, x, y, z);
                 const int l1 = lsm_cell_lin(C.nbx, C.nby, xe, y, z);
                 const uint32_t a = lsm_ld(C.cell_start, l0), b = lsm_ld(C.cell_start, l1 + 1);
@@ -2323,7 +2323,8 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 const int64_t nx = int64_t(std::floor(ext[0] / c)) + 1;
                 const int64_t ny = int64_t(std::floor(ext[1] / c)) + 1;
                 const int64_t nz = int64_t(std::floor(ext[2] / c)) + 1;
-                const int64_t padded = ((nx + 3) / 4) * ((ny + 3) / 4) * ((nz + 3) / 4) * 64;
+                const int64_t padded = ((nx + LSM_BLKX - 1) / LSM_BLKX) * ((ny + 3) / 4) *
+                                       ((nz + 3) / 4) * LSM_BLK_CELLS;
                 if (padded <= MAX_CELLS_PER_CLOUD) {
                     G.nx = int(nx);
                     G.ny = int(ny);
@@ -2338,7 +2339,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         }
         G.cell = c;
         G.inv_cell = 1.f / c;
-        G.nbx = (G.nx + LSM_BLK - 1) / LSM_BLK;
+        G.nbx = (G.nx + LSM_BLKX - 1) / LSM_BLKX;
         G.nby = (G.ny + LSM_BLK - 1) / LSM_BLK;
         G.nbz = (G.nz + LSM_BLK - 1) / LSM_BLK;
         G.ncells = uint32_t(G.nbx) * G.nby * G.nbz * LSM_BLK_CELLS;
