@@ -1320,9 +1320,6 @@ __device__ __forceinline__ float gap2(float q, float lo, float hi) {
 __device__ __forceinline__ int ring_size(int r) { return r == 0 ? 1 : 24 * r * r + 2; }
 __device__ __forceinline__ int ring_prefix(int r) { return r == 0 ? 0 : (2 * r - 1) * (2 * r - 1) * (2 * r - 1); }
 constexpr int FB_R0 = 2;   // the fallback's first shell: rings 0 .. FB_R0 (5 x 5 x 5 blocks)
-#ifndef LSM_FB_BMASK
-#define LSM_FB_BMASK 1     // empty-block test from the block occupancy bits
-#endif
 // the first shell's block offsets (dx, dy, dz) centre-out, by |offset|^2: the blocks nearest the
 // query are scanned first, so the pruning radius shrinks before the outer blocks are tested
 __constant__ int8_t c_shell[3 * 125] = {
@@ -1371,10 +1368,11 @@ __device__ __forceinline__ void ring_offset(int r, int t, int &dx, int &dy, int 
 }
 
 // Exact 1-NN for the queries the box search could not resolve: a group of GL aligned lanes per
-// query (64 / GL queries per wave) walks Chebyshev rings of 4x4x4-cell blocks (each block one
-// contiguous point range) outward from the query's block. Lanes test GL blocks at a time against
-// the current pruning radius (prune2, lower-bound pruning); the surviving blocks are scanned by
-// the whole group. Stops when every unscanned point is provably farther than the best, or than
+// query (64 / GL queries per wave) walks Chebyshev rings of 4x4x4-cell virtual blocks outward
+// from the query's block. Lanes test GL blocks at a time against the current pruning radius
+// (prune2, lower-bound pruning) and the block occupancy bits; the surviving blocks are scanned
+// by the whole group (a block's 16 row ranges pruned by their own lower bounds, compacted by a
+// prefix sum). Stops when every unscanned point is provably farther than the best, or than
 // max_corr. The first shell (rings 0 .. FB_R0, one merge and stop test) is decoded with constant
 // divisors. A first-shell survivor block holds ~14 points, so 32 lanes scan it in one step like
 // 64 do; queries expected to need wide rings take a whole wave (the `far` split).
@@ -1398,8 +1396,11 @@ __device__ __forceinline__ void group_top2(Top2 &t) {
     t.lim = prune2(t.bd2, t.sd2, t.m);
 }
 
+#ifndef LSM_FB_WPE
+#define LSM_FB_WPE 1
+#endif
 template <int GL>
-__global__ void __launch_bounds__(LSM_WAVE)
+__global__ void __launch_bounds__(LSM_WAVE) __attribute__((amdgpu_waves_per_eu(LSM_FB_WPE)))
 nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
               const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
               uint32_t queue_cap, int32_t *__restrict__ corr, int2 *__restrict__ rec, int pass,
@@ -1424,7 +1425,14 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
         transform_point(P.T, lsm_ld(S.xyz, q.i), qx64, qy64, qz64);
         const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
         Top2 t2 = top2_init(q.best, q.best_d2, q.second_d2, q.margin);
-        const float B = G.cell * float(LSM_BLK), Bx = G.cell * float(LSM_BLKX);   // block edges
+        // virtual blocks of 4x4x4 cells: one layout block holds 1 << VBS of them side by side in x;
+        // a virtual block is NR point ranges (its x-chunk of each of its 16 cell rows; one range
+        // when the layout block is itself 4 cells wide)
+        constexpr int VBS = LSM_BLKX_SHIFT - 2;
+        constexpr int NR = LSM_BLKX == 4 ? 1 : 16;
+        constexpr int RL = LSM_BLKX == 4 ? LSM_BLK_CELLS : 4;   // cells per range
+        const int nvbx = G.nbx << VBS;
+        const float B = G.cell * float(LSM_BLK);   // virtual block edge
         const float gx1 = G.ox + G.nx * G.cell, gy1 = G.oy + G.ny * G.cell,
                     gz1 = G.oz + G.nz * G.cell;
         const float box2 = gap2(qx, G.ox, gx1) + gap2(qy, G.oy, gy1) + gap2(qz, G.oz, gz1);
@@ -1435,12 +1443,21 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
             fbound = sqrtf(box2);
             if (sub == 0) fs[6] += 1;
         } else {
-            const float invB = 1.f / B, invBx = 1.f / Bx;
-            const int qbx = (int)floorf((qx - G.ox) * invBx), qby = (int)floorf((qy - G.oy) * invB),
+            const float invB = 1.f / B;
+            const int qbx = (int)floorf((qx - G.ox) * invB), qby = (int)floorf((qy - G.oy) * invB),
                       qbz = (int)floorf((qz - G.oz) * invB);
             auto outside = [](int v, int n) { return v < 0 ? -v : (v > n - 1 ? v - (n - 1) : 0); };
-            const int r0 = max(outside(qbx, G.nbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
+            const int r0 = max(outside(qbx, nvbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
             const uint32_t *cs = G.cell_start;
+            const int gl0 = grp * GL, rr = NR == 1 ? 0 : (sub & 15);
+            // this lane's cell-table word of a virtual block: range rr's start (sub & 16 == 0)
+            // or end
+            const int roff = (NR == 1 ? 0 : (rr >> 2) * 4 * LSM_BLKX + (rr & 3) * LSM_BLKX) +
+                             ((sub >> 4) & 1) * RL;
+            auto vb_word = [&](uint32_t vid) {
+                return lsm_ld(cs, size_t(vid >> VBS) * LSM_BLK_CELLS +
+                                      ((vid & ((1u << VBS) - 1u)) << 2) + uint32_t(roff));
+            };
             int ra = r0, rb = r0 == 0 ? FB_R0 : r0;
             for (;;) {
                 if (sub == 0) fs[1] += 1;
@@ -1449,8 +1466,8 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                 for (int b0 = 0; b0 < nitems; b0 += GL) {
                     if (sub == 0) fs[2] += 1;
                     const int t = b0 + sub;
-                    uint32_t a = 0, b = 0;
-                    float lb = INFINITY;   // lower bound of the block's squared distances
+                    int vid = -1, vby = 0, vbz = 0;
+                    float lb = INFINITY, lbx = 0.f;   // lower bound of the block's squared distances
                     if (t < nitems) {
                         int dx, dy, dz;
                         if (cube) {
@@ -1463,40 +1480,37 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                             ring_offset(r, u, dx, dy, dz);
                         }
                         const int bx = qbx + dx, by = qby + dy, bz = qbz + dz;
-                        if (bx >= 0 && bx < G.nbx && by >= 0 && by < G.nby && bz >= 0 &&
+                        if (bx >= 0 && bx < nvbx && by >= 0 && by < G.nby && bz >= 0 &&
                             bz < G.nbz) {
-                            const float lb2 = gap2(qx, G.ox + bx * Bx, G.ox + (bx + 1) * Bx) +
-                                              gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
+                            lbx = gap2(qx, G.ox + bx * B, G.ox + (bx + 1) * B);
+                            const float lb2 = lbx + gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
                                               gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
-                            if (lb2 * 0.9999f < t2.lim) {
+                            const int bid = (bz * G.nby + by) * nvbx + bx;
+                            // empty blocks (most of a far query's rings) end at the occupancy
+                            // bit, an L1 hit, without cell-table loads
+                            if (lb2 * 0.9999f < t2.lim &&
+                                ((lsm_ld(G.bmask, bid >> 5) >> (bid & 31)) & 1u)) {
                                 lb = lb2;
-                                const int bid = (bz * G.nby + by) * G.nbx + bx;
-#if LSM_FB_BMASK
-                                // empty blocks (most of a far query's rings) end at the
-                                // occupancy bit, an L1 hit, without the cell-table loads
-                                if ((lsm_ld(G.bmask, bid >> 5) >> (bid & 31)) & 1u)
-#endif
-                                {
-                                    a = lsm_ld(cs, size_t(bid) * LSM_BLK_CELLS);
-                                    b = lsm_ld(cs, size_t(bid + 1) * LSM_BLK_CELLS);
-                                }
+                                vid = bid;
+                                vby = by;
+                                vbz = bz;
                             }
                         }
                     }
-                    // survivor blocks one after another; the next block's first points are
-                    // loaded while the current block is tested (a block holds ~14 points, so
-                    // that is usually the whole block)
-                    uint64_t mask = __ballot(b > a) & gmask;
+                    // survivor blocks one after another; the next block's cell-table words are
+                    // loaded while the current block is scanned
+                    uint64_t mask = __ballot(vid >= 0) & gmask;
                     if (mask) {
                         int src = __ffsll((unsigned long long)mask) - 1;
                         mask &= mask - 1;
-                        uint32_t ra_ = __shfl(a, src, LSM_WAVE), rb_ = __shfl(b, src, LSM_WAVE);
-                        float4 p = lsm_ld(G.xyz, min(ra_ + uint32_t(sub), rb_ - 1));
+                        uint32_t cur = uint32_t(__shfl(vid, src, LSM_WAVE));
+                        uint32_t w = vb_word(cur);
+                        int csrc = src;
                         for (;;) {
                             // the next survivor still within the group leader's pruning radius
                             // (it only shrinks; skipping a block beyond one lane's radius leaves
                             // the merged nearest point and rho unchanged, as the first test does)
-                            const float lim0 = __shfl(t2.lim, grp * GL, LSM_WAVE);
+                            const float lim0 = __shfl(t2.lim, gl0, LSM_WAVE);
                             bool more = false;   // uniform in the group
                             while (mask) {
                                 src = __ffsll((unsigned long long)mask) - 1;
@@ -1506,33 +1520,61 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                                     break;
                                 }
                             }
-                            uint32_t na = 0, nb = 0;
-                            float4 pn = p;
-                            if (more) {
-                                na = __shfl(a, src, LSM_WAVE);
-                                nb = __shfl(b, src, LSM_WAVE);
-                                pn = lsm_ld(G.xyz, min(na + uint32_t(sub), nb - 1));
+                            uint32_t wn = w;
+                            if (more) wn = vb_word(uint32_t(__shfl(vid, src, LSM_WAVE)));
+                            // the current block's ranges, each pruned by its rows' lower bound
+                            const uint32_t pa = __shfl(w, gl0 + rr, LSM_WAVE),
+                                           pb = __shfl(w, gl0 + 16 + rr, LSM_WAVE);
+                            uint32_t n = pb - pa;
+                            if (NR > 1) {
+                                const float cx = __shfl(lbx, csrc, LSM_WAVE);
+                                const int y = __shfl(vby, csrc, LSM_WAVE) * 4 + (rr & 3),
+                                          z = __shfl(vbz, csrc, LSM_WAVE) * 4 + (rr >> 2);
+                                const float rlb =
+                                    cx + gap2(qy, G.oy + y * G.cell, G.oy + (y + 1) * G.cell) +
+                                    gap2(qz, G.oz + z * G.cell, G.oz + (z + 1) * G.cell);
+                                if (!(rlb * 0.9999f < lim0)) n = 0;
                             }
+                            uint32_t inc = n;   // inclusive prefix over the 16 ranges
+                            if (NR > 1) {
+#pragma unroll
+                                for (int off = 1; off < 16; off <<= 1) {
+                                    const uint32_t o = __shfl_up(inc, off, 16);
+                                    if (rr >= off) inc += o;
+                                }
+                            }
+                            const uint32_t T = NR > 1 ? __shfl(inc, gl0 + 15, LSM_WAVE) : n;
+                            const uint32_t ex = inc - n;
                             if (sub == 0) {
                                 fs[3] += 1;
-                                fs[4] += rb_ - ra_;
+                                fs[4] += T;
                             }
-                            if (ra_ + uint32_t(sub) < rb_)
-                                top2_add(sqd(p, qx, qy, qz), int(ra_ + uint32_t(sub)), t2);
-                            for (uint32_t k = ra_ + uint32_t(sub + GL); k < rb_; k += GL)
-                                top2_add(sqd(lsm_ld(G.xyz, k), qx, qy, qz), int(k), t2);
+                            for (uint32_t t0 = 0; t0 < T; t0 += GL) {
+                                const uint32_t tt = t0 + uint32_t(sub);
+                                uint32_t k = pa + tt;
+                                if (NR > 1) {   // the range holding point tt (all lanes shuffle)
+                                    int lo = 0;
+#pragma unroll
+                                    for (int step = 8; step > 0; step >>= 1)
+                                        if (__shfl(inc, gl0 + lo + step - 1, LSM_WAVE) <= tt)
+                                            lo += step;
+                                    lo = min(lo, 15);
+                                    k = __shfl(pa, gl0 + lo, LSM_WAVE) +
+                                        (tt - __shfl(ex, gl0 + lo, LSM_WAVE));
+                                }
+                                if (tt < T) top2_add(sqd(lsm_ld(G.xyz, k), qx, qy, qz), int(k), t2);
+                            }
                             if (!more) break;
-                            ra_ = na;
-                            rb_ = nb;
-                            p = pn;
+                            w = wn;
+                            csrc = src;
                         }
                     }
                 }
                 group_top2<GL>(t2);
                 const int r = rb;
                 float bound = INFINITY;
-                if (qbx - r > 0) bound = fminf(bound, qx - (G.ox + (qbx - r) * Bx));
-                if (qbx + r + 1 < G.nbx) bound = fminf(bound, G.ox + (qbx + r + 1) * Bx - qx);
+                if (qbx - r > 0) bound = fminf(bound, qx - (G.ox + (qbx - r) * B));
+                if (qbx + r + 1 < nvbx) bound = fminf(bound, G.ox + (qbx + r + 1) * B - qx);
                 if (qby - r > 0) bound = fminf(bound, qy - (G.oy + (qby - r) * B));
                 if (qby + r + 1 < G.nby) bound = fminf(bound, G.oy + (qby + r + 1) * B - qy);
                 if (qbz - r > 0) bound = fminf(bound, qz - (G.oz + (qbz - r) * B));

@@ -6,9 +6,11 @@
 //     grid row are ONE contiguous point range, and a workgroup of consecutive points covers a
 //     compact patch of space (coherent queries when the cloud is an ICP source);
 //   * a dense CSR cell table cell_start[ncells + 1] (u32) over the cloud's own bounding box, with
-//     cells linearised BLOCKED: 4x4x4-cell blocks in z-major order, cells z-major inside a block.
-//     A block is one contiguous point range (the coarse level the far-field search walks), and
-//     a row of cells inside a block is contiguous too (the fine level);
+//     cells linearised BLOCKED: LSM_BLKX x 4 x 4-cell blocks (x, y, z; 64 x 4 x 4 by default) in
+//     z-major order, cells z-major inside a block. A row of cells inside a block is one
+//     contiguous, x-sorted point range (what the walks scan), and a block's x-chunk of 4 cells
+//     in its 16 rows is a 4x4x4-cell virtual block (the coarse level the far-field search walks,
+//     with an occupancy bit each);
 //   * normals float4 in the same order; perm[] maps sorted position -> reference (filter) order.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -24,11 +26,12 @@ struct CloudDev {
     const float4 *xyz;          // n, cell-sorted
     const float4 *nrm;          // n or nullptr
     const uint32_t *cell_start; // ncells + 1, offsets into xyz
-    const uint32_t *bmask;      // occupancy bit per 4x4x4 block (block id (bz*nby + by)*nbx + bx)
+    const uint32_t *bmask;      // occupancy bit per virtual 4x4x4-cell block (id (bz*nby + by)*nvbx + vbx,
+                                //   nvbx = nbx * LSM_BLKX / 4; grid_fill)
     float ox, oy, oz;           // grid origin
     float cell, inv_cell;       // cell edge and its reciprocal
     int nx, ny, nz;             // cells per axis
-    int nbx, nby, nbz;          // 4x4x4 blocks per axis
+    int nbx, nby, nbz;          // layout blocks per axis (LSM_BLKX, 4, 4 cells)
     int n;
     const uint32_t *perm;       // sorted position -> reference order
     const float4 *prior_ref;    // prior normals in reference order (orientation), or nullptr
@@ -39,11 +42,14 @@ struct CloudDev {
 #define LSM_XYZ_PAD 16     // spare float4 points allocated past every processed cloud's end
 #define LSM_BLK 4          // cells per block edge in y and z
 #define LSM_BLK_SHIFT 2
-// cells per block edge in x: 1 << LSM_BLKX_SHIFT. A row of cells inside a block is one
-// contiguous, x-sorted run, so wider blocks cut the rows the walks visit into fewer runs.
+// cells per block edge in x: 1 << LSM_BLKX_SHIFT (>= 2). A row of cells inside a block is one
+// contiguous, x-sorted run, so wider blocks cut the rows the walks visit into fewer runs
+// (64: C3 7670 -> 8561 pairs/s, profiles/r05o; the correspondence fallback keeps its own
+// 4x4x4-cell virtual blocks, whatever the width).
 #ifndef LSM_BLKX_SHIFT
-#define LSM_BLKX_SHIFT 2
+#define LSM_BLKX_SHIFT 6
 #endif
+static_assert(LSM_BLKX_SHIFT >= 2 && LSM_BLKX_SHIFT <= 8, "x block width 4 .. 256 cells");
 #define LSM_BLKX (1 << LSM_BLKX_SHIFT)
 #define LSM_BLK_CELLS (LSM_BLKX * LSM_BLK * LSM_BLK)
 

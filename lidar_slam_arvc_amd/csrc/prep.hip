@@ -537,10 +537,13 @@ __device__ __forceinline__ uint32_t lower_bound_cell(const uint64_t *k, uint32_t
 }
 
 __global__ void __launch_bounds__(FILL_THREADS)
-grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const *cell_out) {
+grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const *cell_out,
+          uint32_t *const *bm_out) {
+    static_assert(FILL_THREADS == 256 && FILL_TILE % LSM_BLK_CELLS == 0, "virtual-block bits");
     __shared__ uint32_t tile[FILL_TILE];
     __shared__ uint32_t bounds[2];
     __shared__ uint32_t wmin[FILL_THREADS / LSM_WAVE];
+    __shared__ uint32_t vbits[FILL_THREADS / LSM_WAVE];
     const int c = blockIdx.y;
     if (c >= ncloud) return;
     const GridGeo G = geo[c];
@@ -595,30 +598,35 @@ grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const
         __syncthreads();
         for (int e = threadIdx.x; e < FILL_TILE; e += FILL_THREADS)
             if (c0 + e < c1) out[c0 + e] = tile[e];
-        __syncthreads();
-    }
-}
-
-// Block occupancy bits (bit b: block b's 64 cells hold a point), one wave per 64 blocks: the
-// correspondence fallback skips empty blocks without loading their cell-table entries.
-__global__ void __launch_bounds__(256)
-block_mask_kernel(const GridGeo *geo, int ncloud, uint32_t *const *cell_ptrs,
-                  uint32_t *const *bm_ptrs) {
-    const int c = blockIdx.y;
-    if (c >= ncloud) return;
-    const GridGeo G = geo[c];
-    const uint32_t nb = G.ncells / LSM_BLK_CELLS;
-    const uint32_t *cs = cell_ptrs[c];
-    uint32_t *bm = bm_ptrs[c];
-    for (uint32_t b0 = blockIdx.x * 256u; b0 < nb; b0 += gridDim.x * 256u) {
-        const uint32_t b = b0 + threadIdx.x;
-        const bool occ = b < nb && cs[size_t(b + 1) * LSM_BLK_CELLS] > cs[size_t(b) * LSM_BLK_CELLS];
-        const uint64_t m = __ballot(occ);
-        const uint32_t wb = b0 + (threadIdx.x & ~63u);   // this wave's first block
-        if ((threadIdx.x & 63) == 0 && wb < nb) {   // (2 words per 64 blocks are allocated)
-            bm[wb / 32] = uint32_t(m);
-            bm[wb / 32 + 1] = uint32_t(m >> 32);
+        // occupancy bits of the tile's 64 virtual blocks (4x4x4 cells; bit v = layout block
+        // v >> (LSM_BLKX_SHIFT - 2), x-chunk v & (LSM_BLKX / 4 - 1)): thread t tests the x-chunks
+        // of block t / 4's four cell rows at z offset t % 4
+        {
+            constexpr int VBS = LSM_BLKX_SHIFT - 2;
+            const uint32_t vb = threadIdx.x >> 2, zi = threadIdx.x & 3;
+            const uint32_t v = uint32_t(c0 >> 6) + vb;
+            const int64_t cell0 = int64_t(v >> VBS) * LSM_BLK_CELLS +
+                                  ((v & ((1u << VBS) - 1u)) << 2) + zi * 4 * LSM_BLKX - c0;
+            bool occ = false;
+#pragma unroll
+            for (int yi = 0; yi < 4; ++yi) {
+                const int64_t e0 = cell0 + yi * LSM_BLKX, e1 = e0 + 4;
+                const uint32_t a = tile[e0], b = e1 < FILL_TILE ? tile[e1] : p1;
+                occ |= b > a;
+            }
+            uint64_t m = __ballot(occ);
+            m |= m >> 1;
+            m |= m >> 2;   // bit 4 j: block j of this wave's 16
+            uint32_t bits = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) bits |= uint32_t((m >> (4 * j)) & 1u) << j;
+            if (lane == 0) vbits[w] = bits;
+            __syncthreads();
+            if (threadIdx.x < 2)
+                bm_out[c][(c0 >> 11) + threadIdx.x] =
+                    vbits[2 * threadIdx.x] | (vbits[2 * threadIdx.x + 1] << 16);
         }
+        __syncthreads();
     }
 }
 
@@ -2365,7 +2373,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 return LSM_ENOMEM;
             }
         }
-        const int64_t bmw = ((ncells / LSM_BLK_CELLS + 63) / 64) * 2;
+        const int64_t bmw = ncells / 2048 + 2;   // a bit per 64 cells, whole fill tiles
         if (c->bmask_cap < bmw || !c->d_bmask) {
             (void)hipFree(c->d_bmask);
             c->d_bmask = nullptr;
@@ -2441,9 +2449,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     }
     {
         const int gx = int(std::min<int64_t>((maxcells1 + FILL_TILE - 1) / FILL_TILE, 4096));
-        grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs);
-        const int bx = int(std::min<int64_t>((maxcells1 / LSM_BLK_CELLS + 255) / 256, 1024));
-        block_mask_kernel<<<dim3(std::max(bx, 1), K), 256, 0, st>>>(d_geo, K, d_cell_ptrs, d_bm_ptrs);
+        grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs, d_bm_ptrs);
     }
     ctx->toc("grid", ev);
 
