@@ -63,9 +63,9 @@ def source_sha() -> str:
 # The kernels whose machine code a PMC count depends on: the counted kernels and the grid build
 # that lays out what they read (the clouds themselves are pinned bit-exact by the parity tests).
 PMC_KERNELS = {
-    "nn_traffic.json": ("nn_kernel", "grid_keys", "grid_scatter", "grid_fill", "block_mask_kernel"),
+    "nn_traffic.json": ("nn_kernel", "grid_keys", "grid_scatter", "grid_fill"),
     "normals_valu.json": ("normals_sparse_kernel", "normals_dense_kernel", "normals_refine_kernel",
-                          "grid_keys", "grid_scatter", "grid_fill", "block_mask_kernel"),
+                          "grid_keys", "grid_scatter", "grid_fill"),
 }
 
 
