@@ -1396,8 +1396,12 @@ __device__ __forceinline__ void group_top2(Top2 &t) {
     t.lim = prune2(t.bd2, t.sd2, t.m);
 }
 
+#ifndef LSM_FB_U
+#define LSM_FB_U 4        // candidate chunks per round (4 x 32: the whole first shell)
+#endif
+constexpr int FB_U = LSM_FB_U;
 #ifndef LSM_FB_WPE
-#define LSM_FB_WPE 1
+#define LSM_FB_WPE 5      // 94 VGPRs, no spills (6: 10 spilled)
 #endif
 template <int GL>
 __global__ void __launch_bounds__(LSM_WAVE) __attribute__((amdgpu_waves_per_eu(LSM_FB_WPE)))
@@ -1411,13 +1415,21 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
     const int lane = threadIdx.x, sub = lane & (GL - 1), grp = lane / GL;
     const uint64_t gmask = (GL == 64 ? ~0ull : ((1ull << GL) - 1ull)) << (grp * GL);
     const uint32_t total = min(*queue_n, queue_cap);
+    __shared__ int4 s_cand[FB_U][LSM_WAVE];   // candidate block: id, lower bound, y, z
+    __shared__ float s_lbx[FB_U][LSM_WAVE];   // its x part of the lower bound
+    // per-pass statistics (diagnostics builds only: the counters cost registers)
+#ifdef LSM_DIAG
+#define FB_ST(...) __VA_ARGS__
     uint32_t fs[7] = {0, 0, 0, 0, 0, 0, 0};
+#else
+#define FB_ST(...)
+#endif
     for (uint32_t base = blockIdx.x * NG; base < total; base += gridDim.x * NG) {
         const uint32_t it = base + uint32_t(grp);
         if (it >= total) continue;   // whole groups only: the group below stays converged
         const FallbackItem q = queue[it];
         if ((q.best_d2 > far2) != (far != 0)) continue;
-        if (sub == 0) fs[0] += 1;
+        FB_ST(if (sub == 0) fs[0] += 1; const uint32_t chunks0 = fs[2], blocks0 = fs[3];)
         const PairState &P = st[q.pair];
         const CloudDev S = cds[P.src];
         const CloudDev G = cds[P.tgt];
@@ -1441,7 +1453,7 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
             fbound = INFINITY;
         } else if (box2 >= prm.maxc2) {
             fbound = sqrtf(box2);
-            if (sub == 0) fs[6] += 1;
+            FB_ST(if (sub == 0) fs[6] += 1;)
         } else {
             const float invB = 1.f / B;
             const int qbx = (int)floorf((qx - G.ox) * invB), qby = (int)floorf((qy - G.oy) * invB),
@@ -1450,61 +1462,87 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
             const int r0 = max(outside(qbx, nvbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
             const uint32_t *cs = G.cell_start;
             const int gl0 = grp * GL, rr = NR == 1 ? 0 : (sub & 15);
-            // this lane's cell-table word of a virtual block: range rr's start (sub & 16 == 0)
-            // or end
+            // this lane's cell-table words of a virtual block: range rr's start (sub & 16 == 0)
+            // or end; with 16-lane groups both
             const int roff = (NR == 1 ? 0 : (rr >> 2) * 4 * LSM_BLKX + (rr & 3) * LSM_BLKX) +
                              ((sub >> 4) & 1) * RL;
             auto vb_word = [&](uint32_t vid) {
-                return lsm_ld(cs, size_t(vid >> VBS) * LSM_BLK_CELLS +
-                                      ((vid & ((1u << VBS) - 1u)) << 2) + uint32_t(roff));
+                const size_t c = size_t(vid >> VBS) * LSM_BLK_CELLS +
+                                 ((vid & ((1u << VBS) - 1u)) << 2) + uint32_t(roff);
+                return make_uint2(lsm_ld(cs, c), GL == 16 ? lsm_ld(cs, c + RL) : 0u);
             };
             int ra = r0, rb = r0 == 0 ? FB_R0 : r0;
             for (;;) {
-                if (sub == 0) fs[1] += 1;
+                FB_ST(if (sub == 0) fs[1] += 1;)
                 const bool cube = ra == 0;   // rings 0 .. FB_R0 as one (2 FB_R0 + 1)^3 cube
                 const int nitems = ring_prefix(rb + 1) - ring_prefix(ra);
-                for (int b0 = 0; b0 < nitems; b0 += GL) {
-                    if (sub == 0) fs[2] += 1;
-                    const int t = b0 + sub;
-                    int vid = -1, vby = 0, vbz = 0;
-                    float lb = INFINITY, lbx = 0.f;   // lower bound of the block's squared distances
-                    if (t < nitems) {
-                        int dx, dy, dz;
-                        if (cube) {
-                            dx = c_shell[3 * t];
-                            dy = c_shell[3 * t + 1];
-                            dz = c_shell[3 * t + 2];
-                        } else {
-                            int r = ra, u = t;
-                            while (u >= ring_size(r)) u -= ring_size(r++);
-                            ring_offset(r, u, dx, dy, dz);
-                        }
-                        const int bx = qbx + dx, by = qby + dy, bz = qbz + dz;
-                        if (bx >= 0 && bx < nvbx && by >= 0 && by < G.nby && bz >= 0 &&
-                            bz < G.nbz) {
-                            lbx = gap2(qx, G.ox + bx * B, G.ox + (bx + 1) * B);
-                            const float lb2 = lbx + gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
-                                              gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
-                            const int bid = (bz * G.nby + by) * nvbx + bx;
+                // FB_U chunks of GL candidates per round: their occupancy-bit loads are in
+                // flight together; the candidates wait in LDS for the survivor scan
+                for (int b0 = 0; b0 < nitems; b0 += GL * FB_U) {
+                    uint64_t masks[FB_U];
+                    {
+                        int bid_[FB_U];
+                        uint32_t bw[FB_U];
+#pragma unroll
+                        for (int u = 0; u < FB_U; ++u) {
+                            FB_ST(if (sub == 0 && b0 + u * GL < nitems) fs[2] += 1;)
+                            const int t = b0 + u * GL + sub;
+                            bid_[u] = -1;
+                            int by_ = 0, bz_ = 0;
+                            float lb_ = INFINITY;   // lower bound of the block's squared distances
+                            float lbx_ = 0.f;
+                            bw[u] = 0u;
+                            if (t < nitems) {
+                                int dx, dy, dz;
+                                if (cube) {
+                                    dx = c_shell[3 * t];
+                                    dy = c_shell[3 * t + 1];
+                                    dz = c_shell[3 * t + 2];
+                                } else {
+                                    int r = ra, v = t;
+                                    while (v >= ring_size(r)) v -= ring_size(r++);
+                                    ring_offset(r, v, dx, dy, dz);
+                                }
+                                const int bx = qbx + dx, by = qby + dy, bz = qbz + dz;
+                                if (bx >= 0 && bx < nvbx && by >= 0 && by < G.nby && bz >= 0 &&
+                                    bz < G.nbz) {
+                                    const float gx = gap2(qx, G.ox + bx * B, G.ox + (bx + 1) * B);
+                                    const float lb2 =
+                                        gx + gap2(qy, G.oy + by * B, G.oy + (by + 1) * B) +
+                                        gap2(qz, G.oz + bz * B, G.oz + (bz + 1) * B);
+                                    if (lb2 * 0.9999f < t2.lim) {
+                                        bid_[u] = (bz * G.nby + by) * nvbx + bx;
+                                        by_ = by;
+                                        bz_ = bz;
+                                        lb_ = lb2;
+                                        lbx_ = gx;
+                                    }
+                                }
+                            }
                             // empty blocks (most of a far query's rings) end at the occupancy
                             // bit, an L1 hit, without cell-table loads
-                            if (lb2 * 0.9999f < t2.lim &&
-                                ((lsm_ld(G.bmask, bid >> 5) >> (bid & 31)) & 1u)) {
-                                lb = lb2;
-                                vid = bid;
-                                vby = by;
-                                vbz = bz;
-                            }
+                            if (bid_[u] >= 0) bw[u] = lsm_ld(G.bmask, bid_[u] >> 5);
+                            s_cand[u][lane] = make_int4(bid_[u], __float_as_int(lb_), by_, bz_);
+                            s_lbx[u][lane] = lbx_;
                         }
+#pragma unroll
+                        for (int u = 0; u < FB_U; ++u)
+                            masks[u] = __ballot(bid_[u] >= 0 && ((bw[u] >> (bid_[u] & 31)) & 1u)) &
+                                       gmask;
+                        // the wave's own LDS writes, read back by other lanes below
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                     }
+#pragma unroll
+                    for (int u = 0; u < FB_U; ++u) {
                     // survivor blocks one after another; the next block's cell-table words are
                     // loaded while the current block is scanned
-                    uint64_t mask = __ballot(vid >= 0) & gmask;
+                    uint64_t mask = masks[u];
                     if (mask) {
                         int src = __ffsll((unsigned long long)mask) - 1;
                         mask &= mask - 1;
-                        uint32_t cur = uint32_t(__shfl(vid, src, LSM_WAVE));
-                        uint32_t w = vb_word(cur);
+                        uint2 w = vb_word(uint32_t(s_cand[u][src].x));
                         int csrc = src;
                         for (;;) {
                             // the next survivor still within the group leader's pruning radius
@@ -1515,21 +1553,21 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                             while (mask) {
                                 src = __ffsll((unsigned long long)mask) - 1;
                                 mask &= mask - 1;
-                                if (__shfl(lb, src, LSM_WAVE) * 0.9999f < lim0) {
+                                if (__int_as_float(s_cand[u][src].y) * 0.9999f < lim0) {
                                     more = true;
                                     break;
                                 }
                             }
-                            uint32_t wn = w;
-                            if (more) wn = vb_word(uint32_t(__shfl(vid, src, LSM_WAVE)));
+                            uint2 wn = w;
+                            if (more) wn = vb_word(uint32_t(s_cand[u][src].x));
                             // the current block's ranges, each pruned by its rows' lower bound
-                            const uint32_t pa = __shfl(w, gl0 + rr, LSM_WAVE),
-                                           pb = __shfl(w, gl0 + 16 + rr, LSM_WAVE);
+                            const uint32_t pa = GL == 16 ? w.x : __shfl(w.x, gl0 + rr, LSM_WAVE),
+                                           pb = GL == 16 ? w.y : __shfl(w.x, gl0 + 16 + rr, LSM_WAVE);
                             uint32_t n = pb - pa;
                             if (NR > 1) {
-                                const float cx = __shfl(lbx, csrc, LSM_WAVE);
-                                const int y = __shfl(vby, csrc, LSM_WAVE) * 4 + (rr & 3),
-                                          z = __shfl(vbz, csrc, LSM_WAVE) * 4 + (rr >> 2);
+                                const int4 cc = s_cand[u][csrc];
+                                const float cx = s_lbx[u][csrc];
+                                const int y = cc.z * 4 + (rr & 3), z = cc.w * 4 + (rr >> 2);
                                 const float rlb =
                                     cx + gap2(qy, G.oy + y * G.cell, G.oy + (y + 1) * G.cell) +
                                     gap2(qz, G.oz + z * G.cell, G.oz + (z + 1) * G.cell);
@@ -1545,10 +1583,10 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                             }
                             const uint32_t T = NR > 1 ? __shfl(inc, gl0 + 15, LSM_WAVE) : n;
                             const uint32_t ex = inc - n;
-                            if (sub == 0) {
+                            FB_ST(if (sub == 0) {
                                 fs[3] += 1;
                                 fs[4] += T;
-                            }
+                            })
                             for (uint32_t t0 = 0; t0 < T; t0 += GL) {
                                 const uint32_t tt = t0 + uint32_t(sub);
                                 uint32_t k = pa + tt;
@@ -1568,6 +1606,7 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                             w = wn;
                             csrc = src;
                         }
+                    }
                     }
                 }
                 group_top2<GL>(t2);
@@ -1591,14 +1630,17 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
         if (sub == 0) {
             const int64_t g = P.src_off + q.i;
             const bool hit = t2.bidx >= 0 && t2.bd2 < prm.maxc2;
-            fs[5] += hit ? 1 : 0;
+            FB_ST(fs[5] += hit ? 1 : 0;)
             corr[g] = hit ? t2.bidx : -1;
             rec[g] = rec_pack(-1, pass, hit ? rho_from(t2.lim, fbound) : rho_from(t2.bd2, fbound));
+            FB_ST(if (fstats)   // the pass's costliest item: chunks << 32 | survivor blocks
+                atomicMax(fstats + 7, ((unsigned long long)(fs[2] - chunks0) << 32) |
+                                          (unsigned long long)(fs[3] - blocks0));)
         }
     }
-    if (fstats && sub == 0)
-        for (int c = 0; c < 7; ++c)
-            if (fs[c]) atomicAdd(fstats + c, (unsigned long long)fs[c]);
+    FB_ST(if (fstats && sub == 0) for (int c = 0; c < 7; ++c) if (fs[c])
+              atomicAdd(fstats + c, (unsigned long long)fs[c]);)
+#undef FB_ST
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2142,7 +2184,10 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             for (int k = 0; k < n; ++k) ctx->event_pool.push_back(ev[size_t(k)]);
         }
     } ev_return{ctx, pass_ev, passes};
-    const int fb_grid = std::max(1, std::min(ctx->num_cus * 16, 8192));
+    // the fallback: GL lanes per queued query (LSM_FB_GL 16 / 32), LSM_FB_WAVES one-wave
+    // workgroups per CU (grid-stride over the queue)
+    const int fb_gl = int(lsm_knob("LSM_FB_GL", 32));
+    const int fb_grid = std::max(1, std::min(ctx->num_cus * int(lsm_knob("LSM_FB_WAVES", 20)), 16384));
     const int box_grid = std::max(1, ctx->num_cus * 8);   // nn_box_kernel: grid-stride
     constexpr int PASS_LAG = 2;   // passes queued ahead of the last one read back
     // LSM_NN_NOCERT=1: search every query in every pass (no stability certificate) -- the
@@ -2232,8 +2277,12 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         {
             unsigned long long *fst = d_nst ? d_nst + size_t(ncnt) * NN_NSTAT + size_t(pass) * 8
                                             : nullptr;
-            nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
-                                                            qcap, d_corr, d_rec, pass, fst, INFINITY, 0);
+            if (fb_gl == 16)
+                nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                qcap, d_corr, d_rec, pass, fst, INFINITY, 0);
+            else
+                nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                qcap, d_corr, d_rec, pass, fst, INFINITY, 0);
         }
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);
@@ -2278,8 +2327,9 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
             const double fq = double(std::max(f[0], 1ull));
             fprintf(stderr,
                     "fbstat pass %2d: queries %8llu rings %.2f chunks %.2f blocks %.2f points "
-                    "%.1f hits %.3f outside %.3f\n",
-                    k, f[0], f[1] / fq, f[2] / fq, f[3] / fq, f[4] / fq, f[5] / fq, f[6] / fq);
+                    "%.1f hits %.3f outside %.3f max-item chunks %llu blocks %llu\n",
+                    k, f[0], f[1] / fq, f[2] / fq, f[3] / fq, f[4] / fq, f[5] / fq, f[6] / fq,
+                    f[7] >> 32, f[7] & 0xffffffffull);
         }
     }
     double nn_bytes = 0.0;
