@@ -26,7 +26,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CELL = np.float32(0.375)
-BLK = 4
+BLK = 4           # cells per layout block edge in y and z
+BLKX = 64         # ... and in x (lsm_common.h LSM_BLKX)
 LIN = 8            # runs of at most this many points are scanned whole
 KCOLD, KMAX = 4, 4
 INF = np.float32(np.inf)
@@ -41,21 +42,21 @@ class Grid:
         self.inv = np.float32(1.0) / CELL
         ext = p.max(axis=0) - self.o
         self.n = (np.floor(ext / CELL).astype(np.int64) + 1)
-        self.nb = (self.n + BLK - 1) // BLK
+        self.nb = (self.n + np.array([BLKX, BLK, BLK]) - 1) // np.array([BLKX, BLK, BLK])
         c = np.floor((p - self.o) * self.inv).astype(np.int64)
         c = np.minimum(np.maximum(c, 0), self.n - 1)
         lin = self.lin(c[:, 0], c[:, 1], c[:, 2])
         order = np.lexsort((p[:, 0], lin))
         self.p = p[order]
         self.x = self.p[:, 0]
-        ncell = int(self.nb[0] * self.nb[1] * self.nb[2] * 64)
+        ncell = int(self.nb[0] * self.nb[1] * self.nb[2] * BLKX * BLK * BLK)
         cnt = np.bincount(lin, minlength=ncell)
         self.cs = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
 
     def lin(self, x, y, z):
-        bx, by, bz = x >> 2, y >> 2, z >> 2
-        return (((bz * self.nb[1] + by) * self.nb[0] + bx) << 6) | ((z & 3) << 4) | \
-               ((y & 3) << 2) | (x & 3)
+        bx, by, bz = x // BLKX, y >> 2, z >> 2
+        return (((bz * self.nb[1] + by) * self.nb[0] + bx) * (BLKX * 16)) + ((z & 3) * 4 * BLKX) + \
+               ((y & 3) * BLKX) + (x % BLKX)
 
 
 def sqd(t, q):
@@ -142,7 +143,7 @@ def query(G, q, prev, m, st):
                 xb = min(xb, math.floor(f[0] + ch))
             x = xa
             while x <= xb:
-                xe = min(xb, x | (BLK - 1))
+                xe = min(xb, x | (BLKX - 1))
                 a, b = G.cs[G.lin(x, y, z)], G.cs[G.lin(xe, y, z) + 1]
                 st["parts"] += 1
                 if b > a:
