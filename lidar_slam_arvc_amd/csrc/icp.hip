@@ -1449,6 +1449,11 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                     gz1 = G.oz + G.nz * G.cell;
         const float box2 = gap2(qx, G.ox, gx1) + gap2(qy, G.oy, gy1) + gap2(qz, G.oz, gz1);
         float fbound = 0.f;
+#if LSM_FB_PROBE == 1   // timing probe (diagnostics only, wrong results): item setup alone
+        if (G.n > 0) {
+            fbound = 0.f;
+        } else
+#endif
         if (G.n <= 0) {
             fbound = INFINITY;
         } else if (box2 >= prm.maxc2) {
@@ -1538,7 +1543,11 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
                     for (int u = 0; u < FB_U; ++u) {
                     // survivor blocks one after another; the next block's cell-table words are
                     // loaded while the current block is scanned
+#if LSM_FB_PROBE == 2   // timing probe (diagnostics only, wrong results): no survivor scans
+                    uint64_t mask = 0 & masks[u];
+#else
                     uint64_t mask = masks[u];
+#endif
                     if (mask) {
                         int src = __ffsll((unsigned long long)mask) - 1;
                         mask &= mask - 1;
