@@ -22,7 +22,7 @@ static const char *kVersion = "liblidarsm 0.1 (gfx950)";
 static const char *const kKnobs[] = {
     "LSM_NN_SPLIT",  "LSM_NN_SPLIT_PLACE", "LSM_NN_NOCERT", "LSM_NN_CERT_FROM",  "LSM_NN_DIRECT",
     "LSM_NN_DIRECT_ITER", "LSM_NN_KCOLD", "LSM_NN_KMAX",   "LSM_NN_COLD_SEED",  "LSM_NORMALS_EXACT",
-    "LSM_NORMALS_SPLIT", "LSM_NN_TILE", "LSM_NN_FULL_L", "LSM_FB_GL", "LSM_FB_WAVES"};
+    "LSM_NORMALS_SPLIT", "LSM_NN_TILE", "LSM_NN_FULL_L", "LSM_FB_GL", "LSM_FB_WAVES", "LSM_FB_WIDE_FROM", "LSM_FB_FAR", "LSM_FB_WIDE_MAX", "LSM_FB_WIDE_MAXC"};
 
 double lsm_knob(const char *name, double dflt) {
     bool known = false;

@@ -1404,19 +1404,18 @@ constexpr int FB_U = LSM_FB_U;
 #define LSM_FB_WPE 5      // 94 VGPRs, no spills (6: 10 spilled)
 #endif
 template <int GL>
-__global__ void __launch_bounds__(LSM_WAVE) __attribute__((amdgpu_waves_per_eu(LSM_FB_WPE)))
-nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
-              const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
-              uint32_t queue_cap, int32_t *__restrict__ corr, int2 *__restrict__ rec, int pass,
-              unsigned long long *__restrict__ fstats, float far2, int far) {
+__device__ __forceinline__ void
+fallback_run(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, const NNParams &prm,
+             const FallbackItem *__restrict__ queue, uint32_t total, int32_t *__restrict__ corr,
+             int2 *__restrict__ rec, int pass, unsigned long long *__restrict__ fstats, float far2,
+             int far, int4 (*__restrict__ s_cand)[LSM_WAVE], float (*__restrict__ s_lbx)[LSM_WAVE]) {
     // far = 0: the items whose box-search best is within sqrt(far2) (or all when far2 = inf);
     // far = 1: the others (expected to need wider rings: more lanes per query)
+    // s_cand / s_lbx: the wave's LDS candidate slots ([FB_U][64]: block id, lower bound, y, z /
+    // the x part of the lower bound)
     constexpr int NG = LSM_WAVE / GL;
     const int lane = threadIdx.x, sub = lane & (GL - 1), grp = lane / GL;
     const uint64_t gmask = (GL == 64 ? ~0ull : ((1ull << GL) - 1ull)) << (grp * GL);
-    const uint32_t total = min(*queue_n, queue_cap);
-    __shared__ int4 s_cand[FB_U][LSM_WAVE];   // candidate block: id, lower bound, y, z
-    __shared__ float s_lbx[FB_U][LSM_WAVE];   // its x part of the lower bound
     // per-pass statistics (diagnostics builds only: the counters cost registers)
 #ifdef LSM_DIAG
 #define FB_ST(...) __VA_ARGS__
@@ -1650,6 +1649,36 @@ nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds
     FB_ST(if (fstats && sub == 0) for (int c = 0; c < 7; ++c) if (fs[c])
               atomicAdd(fstats + c, (unsigned long long)fs[c]);)
 #undef FB_ST
+}
+
+template <int GL>
+__global__ void __launch_bounds__(LSM_WAVE) __attribute__((amdgpu_waves_per_eu(LSM_FB_WPE)))
+nn_fallback_g(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
+              const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
+              uint32_t queue_cap, int32_t *__restrict__ corr, int2 *__restrict__ rec, int pass,
+              unsigned long long *__restrict__ fstats, float far2, int far) {
+    __shared__ int4 s_cand[FB_U][LSM_WAVE];
+    __shared__ float s_lbx[FB_U][LSM_WAVE];
+    fallback_run<GL>(st, cds, prm, queue, min(*queue_n, queue_cap), corr, rec, pass, fstats, far2,
+                     far, s_cand, s_lbx);
+}
+
+// The fallback with its lanes per query chosen on the device from the pass's queue length: a
+// whole wave per query for a queue of at most wide_max (the later passes, and the few but far
+// queries of revisit pairs), 32 lanes for a longer one (the first passes of a sequence, where two
+// queries per wave keep more of them in flight).
+__global__ void __launch_bounds__(LSM_WAVE) __attribute__((amdgpu_waves_per_eu(LSM_FB_WPE)))
+nn_fallback_auto(const PairState *__restrict__ st, const CloudDev *__restrict__ cds, NNParams prm,
+                 const FallbackItem *__restrict__ queue, const uint32_t *__restrict__ queue_n,
+                 uint32_t queue_cap, int32_t *__restrict__ corr, int2 *__restrict__ rec, int pass,
+                 unsigned long long *__restrict__ fstats, uint32_t wide_max) {
+    __shared__ int4 s_cand[FB_U][LSM_WAVE];
+    __shared__ float s_lbx[FB_U][LSM_WAVE];
+    const uint32_t total = min(*queue_n, queue_cap);
+    if (total <= wide_max)
+        fallback_run<64>(st, cds, prm, queue, total, corr, rec, pass, fstats, INFINITY, 0, s_cand, s_lbx);
+    else
+        fallback_run<32>(st, cds, prm, queue, total, corr, rec, pass, fstats, INFINITY, 0, s_cand, s_lbx);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2195,7 +2224,15 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     } ev_return{ctx, pass_ev, passes};
     // the fallback: GL lanes per queued query (LSM_FB_GL 16 / 32), LSM_FB_WAVES one-wave
     // workgroups per CU (grid-stride over the queue)
-    const int fb_gl = int(lsm_knob("LSM_FB_GL", 32));
+    // LSM_FB_GL 0 (default): chosen per pass on the device (nn_fallback_auto, LSM_FB_WIDE_MAX)
+    const int fb_gl = int(lsm_knob("LSM_FB_GL", 0));
+    // whole-wave queries only where the fallback can search far: max_corr >= LSM_FB_WIDE_MAXC m
+    // (C3 / C4's 10 m; a multi-scale ladder's <= 2 m searches are short and cheaper at 32 lanes)
+    const uint32_t fb_wide_max =
+        p.max_correspondence_distance >= lsm_knob("LSM_FB_WIDE_MAXC", 4.0)
+            ? uint32_t(lsm_knob("LSM_FB_WIDE_MAX", 200000)) : 0u;
+    const int fb_wide_from = int(lsm_knob("LSM_FB_WIDE_FROM", 1 << 20));   // GL 64 from this pass
+    const float fb_far = float(lsm_knob("LSM_FB_FAR", 0.0));   // far split (m; 0: off)
     const int fb_grid = std::max(1, std::min(ctx->num_cus * int(lsm_knob("LSM_FB_WAVES", 20)), 16384));
     const int box_grid = std::max(1, ctx->num_cus * 8);   // nn_box_kernel: grid-stride
     constexpr int PASS_LAG = 2;   // passes queued ahead of the last one read back
@@ -2286,8 +2323,29 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         {
             unsigned long long *fst = d_nst ? d_nst + size_t(ncnt) * NN_NSTAT + size_t(pass) * 8
                                             : nullptr;
-            if (fb_gl == 16)
+            // from pass fb_wide_from on (the non-converging pairs' tail: few, costly queries) a
+            // whole wave per query
+            const int gl = pass >= fb_wide_from ? 64 : fb_gl;
+            if (fb_gl == 0 && pass < fb_wide_from) {
+                nn_fallback_auto<<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass, qcap,
+                                                               d_corr, d_rec, pass, fst, fb_wide_max);
+            } else if (gl != 64 && fb_far > 0.f) {
+                // the far split: queries whose box-search best lies beyond fb_far (or that have
+                // none) take a whole wave, the rest GL lanes
+                const float f2 = fb_far * fb_far;
+                if (gl == 16)
+                    nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                    qcap, d_corr, d_rec, pass, fst, f2, 0);
+                else
+                    nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                    qcap, d_corr, d_rec, pass, fst, f2, 0);
+                nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                qcap, d_corr, d_rec, pass, fst, f2, 1);
+            } else if (gl == 16)
                 nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                                                                qcap, d_corr, d_rec, pass, fst, INFINITY, 0);
+            else if (gl == 64)
+                nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
                                                                 qcap, d_corr, d_rec, pass, fst, INFINITY, 0);
             else
                 nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,

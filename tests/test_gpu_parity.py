@@ -453,7 +453,10 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monk
                                  {"LSM_NN_FULL_L": "2", "LSM_NN_NOCERT": "1"},
                                  {"LSM_FB_GL": "16"}, {"LSM_FB_GL": "16", "LSM_NN_DIRECT": "1",
                                                        "LSM_NN_DIRECT_ITER": "0"},
-                                 {"LSM_FB_WAVES": "3"}])
+                                 {"LSM_FB_WAVES": "3"}, {"LSM_FB_WIDE_FROM": "0"},
+                                 {"LSM_FB_WIDE_FROM": "2"}, {"LSM_FB_FAR": "1.5"},
+                                 {"LSM_FB_FAR": "0.5", "LSM_FB_GL": "16"}, {"LSM_FB_GL": "32"},
+                                 {"LSM_FB_WIDE_MAX": "0"}, {"LSM_FB_WIDE_MAX": "4000000000"}])
 def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     """The exact 1-NN may be reached along different paths: the stability check from pass 1, 2
     or 4, queries with a
@@ -463,7 +466,9 @@ def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     split groups placed anywhere in the workgroup, cold searches seeded with a point of the
     query's own cell (default) or not, the full passes' searches from global memory (default) or
     from LDS-staged target tiles (LSM_NN_TILE=1: nn_tile_kernel + nn_box_kernel), the fallback
-    with 16 or 32 (default) lanes per query and any grid size. Every choice
+    with 16, 32 or 64 lanes per query (chosen per pass from the queue length -- the default --, 64
+    from any pass on, or for the queries whose box-search best lies beyond a distance) and any
+    grid size. Every choice
     must give the same correspondences, so every result is bit-identical to the default's
     (C4-style revisit pairs: large initial errors, many fallback queries)."""
     ps = synthetic.make_revisit_pairs(6, seed=41, model=synthetic.HDL64)

@@ -6,7 +6,7 @@ set -u
 OUT=gpurun_out/pmc_fb; mkdir -p $OUT; export TMPDIR=/tmp
 ARGS="--workload hdl64_seq --steps 1 --warmup 1 --no-cpu-baseline --no-c1 --no-c45 --seq-cache /tmp/lsm_hdl64_seq.npz"
 [ -f /tmp/lsm_hdl64_seq.npz ] || timeout -k 10 300 python bench.py $ARGS > $OUT/plain.log 2>&1 || { echo "plain run failed"; exit 1; }
-RX="nn_fallback_g"
+RX="nn_fallback"
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" \
            "TA_TA_BUSY_sum TA_BUFFER_TOTAL_CYCLES_sum GRBM_GUI_ACTIVE GRBM_COUNT" \
@@ -25,7 +25,7 @@ for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
 durs = []
 for f in glob.glob(out + "/p1/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "nn_fallback_g" in r["Kernel_Name"]:
+        if "nn_fallback" in r["Kernel_Name"]:
             durs.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
 durs = [d for _, d in sorted(durs)]
 res = {"counters_per_step_2": dict(agg), "launch_us": durs}
