@@ -811,8 +811,14 @@ __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, fl
 // One x-sorted run [a, b) of a row with its window [xl, xh]: body(p, k) for every point in the
 // window. Long runs find the window's first point by binary search on x (a run averages ~140
 // points of which ~30 lie left of the window on HDL-64 scans); the walk stops past xh.
-constexpr uint32_t SCAN_BSEARCH = 16;
-constexpr uint32_t SCAN_SLACK = 8;   // scan_run_pred: entry search stops within this many points
+#ifndef LSM_SCAN_BSEARCH
+#define LSM_SCAN_BSEARCH 16
+#endif
+#ifndef LSM_SCAN_SLACK
+#define LSM_SCAN_SLACK 8
+#endif
+constexpr uint32_t SCAN_BSEARCH = LSM_SCAN_BSEARCH;
+constexpr uint32_t SCAN_SLACK = LSM_SCAN_SLACK;   // scan_run_pred: entry search stops within this many points
 // points per load group of the normals walks, and whether the next group's loads are issued
 // before the current group is tested (measured per 65 keyframes: G4 6.65 ms, G2 + prefetch 6.43,
 // G4 + prefetch 7.57 -- the extra registers cost occupancy)
