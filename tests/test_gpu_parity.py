@@ -456,7 +456,8 @@ def test_certified_split_searches_bit_identical_on_bench_sequence(dev, env, monk
                                  {"LSM_FB_WAVES": "3"}, {"LSM_FB_WIDE_FROM": "0"},
                                  {"LSM_FB_WIDE_FROM": "2"}, {"LSM_FB_FAR": "1.5"},
                                  {"LSM_FB_FAR": "0.5", "LSM_FB_GL": "16"}, {"LSM_FB_GL": "32"},
-                                 {"LSM_FB_WIDE_MAX": "0"}, {"LSM_FB_WIDE_MAX": "4000000000"}])
+                                 {"LSM_FB_WIDE_MAX": "0"}, {"LSM_FB_WIDE_MAX": "4000000000"},
+                                 {"LSM_FB_WIDE_MAXC": "100"}])
 def test_search_path_variants_bit_identical(dev, env, monkeypatch):
     """The exact 1-NN may be reached along different paths: the stability check from pass 1, 2
     or 4, queries with a
