@@ -499,22 +499,17 @@ grid_keys(const Seg *segs, const float4 *pts, const GridGeo *geo, uint64_t *keys
 
 __global__ void __launch_bounds__(PT_THREADS)
 grid_scatter(const Seg *segs, const GridGeo *geo, const CloudDev *cd, const uint32_t *svals,
-             const uint64_t *skeys, const float4 *pts, uint32_t *const *perm_out,
-             uint32_t *nonempty) {
+             const float4 *pts, uint32_t *const *perm_out) {
     const Seg s = segs[blockIdx.x];
     const GridGeo G = geo[s.cloud];
     const int j = s.start + threadIdx.x;
-    bool head = false;
     if (j < int(G.n)) {
         const uint32_t g = G.pt_off + j;
         const uint32_t v = svals[g];
         float4 *xyz = const_cast<float4 *>(cd[s.cloud].xyz);
         xyz[j] = pts[v];
         perm_out[s.cloud][j] = v - G.pt_off;   // reference (filter / voxel-key) order
-        head = (j == 0) || ((skeys[g] >> 32) != (skeys[g - 1] >> 32));
     }
-    uint64_t m = __ballot(head);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&nonempty[s.cloud], (uint32_t)__popcll(m));
 }
 
 // cell_start[c] = first sorted position with key >= c (lower bound), for c in [0, ncells].
@@ -538,7 +533,7 @@ __device__ __forceinline__ uint32_t lower_bound_cell(const uint64_t *k, uint32_t
 
 __global__ void __launch_bounds__(FILL_THREADS)
 grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const *cell_out,
-          uint32_t *const *bm_out) {
+          uint32_t *const *bm_out, uint32_t *nonempty) {
     static_assert(FILL_THREADS == 256 && FILL_TILE % LSM_BLK_CELLS == 0, "virtual-block bits");
     __shared__ uint32_t tile[FILL_TILE];
     __shared__ uint32_t bounds[2];
@@ -560,10 +555,17 @@ grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const
         const uint32_t p0 = bounds[0], p1 = bounds[1];
         for (int e = threadIdx.x; e < FILL_TILE; e += FILL_THREADS) tile[e] = p1;
         __syncthreads();
+        uint32_t heads = 0;   // occupied cells of the tile (the cloud's count: bench bytes)
         for (uint32_t j = p0 + threadIdx.x; j < p1; j += FILL_THREADS) {
             const uint32_t cj = uint32_t(k[j] >> 32);
-            if (j == 0 || uint32_t(k[j - 1] >> 32) != cj) tile[cj - G.cell_off - uint32_t(c0)] = j;
+            if (j == 0 || uint32_t(k[j - 1] >> 32) != cj) {
+                tile[cj - G.cell_off - uint32_t(c0)] = j;
+                ++heads;
+            }
         }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) heads += __shfl_xor(heads, off, LSM_WAVE);
+        if (lane == 0 && heads) atomicAdd(&nonempty[c], heads);
         __syncthreads();
         // backward min-scan: thread t owns cells [16 t, 16 t + 16)
         uint32_t v[FILL_PER];
@@ -2450,12 +2452,13 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         void *tmp = ctx->buf("sort_tmp", tmpb);
         LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<uint64_t>>(tmp, tmpb, k_in, k_out, v_in, v_out,
                                                                    size_t(ntot), 0, endbit, st));
-        grid_scatter<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_geo, d_cd, v_out, k_out,
-                                                              wpts, d_perm_ptrs, nonempty);
+        grid_scatter<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_geo, d_cd, v_out, wpts,
+                                                              d_perm_ptrs);
     }
     {
         const int gx = int(std::min<int64_t>((maxcells1 + FILL_TILE - 1) / FILL_TILE, 4096));
-        grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs, d_bm_ptrs);
+        grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs, d_bm_ptrs,
+                                                        nonempty);
     }
     ctx->toc("grid", ev);
 
