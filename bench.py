@@ -534,9 +534,12 @@ def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda
             # PMC count of the same workload and normals mode (profiles/normals_valu.json)
             vj, v_why = pmc_entry("normals_valu.json", workload, P, normals)
             if vj:
-                valu = vj.get("valu_per_step")
-                pk = vj.get("per_kernel_per_step", {})
+                # the refine kernel (0.2 % of the VALU) runs on the library's side stream,
+                # overlapping the ICP, outside the timed normals windows: left out of the count too
+                pk = {k: v for k, v in vj.get("per_kernel_per_step", {}).items()
+                      if k != "normals_refine_kernel"}
                 valu_k = {k: v.get("SQ_INSTS_VALU") for k, v in pk.items()}
+                valu = sum(v or 0.0 for v in valu_k.values()) if valu_k else vj.get("valu_per_step")
                 f64 = sum(v.get("SQ_INSTS_VALU_ADD_F64", 0.0) + v.get("SQ_INSTS_VALU_FMA_F64", 0.0)
                           for v in pk.values())
             ach = valu / step_s / 1e9 if valu else None
@@ -544,8 +547,9 @@ def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda
             # other f64 instructions -- mul, conversions, compares -- are counted at the f32 rate)
             t_peak = ((valu - f64) / (VALU_ISSUE_PEAK_G * 1e9) + f64 / (VALU_F64_PEAK_G * 1e9)
                       if valu and f64 is not None else None)
-            roof_n = {"bound": "valu", "kernel": "normals_sparse_kernel + normals_dense_kernel + "
-                                                 "normals_refine_kernel (the split launch; " +
+            roof_n = {"bound": "valu", "kernel": "normals_sparse_kernel + normals_dense_kernel "
+                                                 "(the split launch, its refine kernel overlapped "
+                                                 "with the ICP on a side stream; " +
                                                  ("each keyframe's normals when it is first a "
                                                   "P2Plane target" if normals == "lazy" else
                                                   "every keyframe, once per step") +

@@ -22,7 +22,7 @@ static const char *kVersion = "liblidarsm 0.1 (gfx950)";
 static const char *const kKnobs[] = {
     "LSM_NN_SPLIT",  "LSM_NN_SPLIT_PLACE", "LSM_NN_NOCERT", "LSM_NN_CERT_FROM",  "LSM_NN_DIRECT",
     "LSM_NN_DIRECT_ITER", "LSM_NN_KCOLD", "LSM_NN_KMAX",   "LSM_NN_COLD_SEED",  "LSM_NORMALS_EXACT",
-    "LSM_NORMALS_SPLIT", "LSM_NN_TILE", "LSM_NN_FULL_L", "LSM_FB_GL", "LSM_FB_WAVES", "LSM_FB_WIDE_FROM", "LSM_FB_FAR", "LSM_FB_WIDE_MAX", "LSM_FB_WIDE_MAXC"};
+    "LSM_NORMALS_SPLIT", "LSM_NORMALS_SIDE", "LSM_NN_TILE", "LSM_NN_FULL_L", "LSM_FB_GL", "LSM_FB_WAVES", "LSM_FB_WIDE_FROM", "LSM_FB_FAR", "LSM_FB_WIDE_MAX", "LSM_FB_WIDE_MAXC"};
 
 double lsm_knob(const char *name, double dflt) {
     bool known = false;
@@ -40,6 +40,7 @@ void *lsm_ctx::buf(const std::string &name, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.bytes < bytes) {
         if (b.p) {
+            if (side) (void)hipStreamSynchronize(side);
             (void)hipStreamSynchronize(stream);
             (void)hipFree(b.p);
             b.p = nullptr;
@@ -87,23 +88,28 @@ hipEvent_t lsm_ctx::get_event() {
     return e;
 }
 
-void lsm_ctx::tic(const char *name, hipEvent_t *a) {
+void lsm_ctx::tic(const char *name, hipEvent_t *a, hipStream_t on) {
     (void)name;
     *a = nullptr;
     if (!timing) return;
     *a = get_event();
-    (void)hipEventRecord(*a, stream);
+    (void)hipEventRecord(*a, on ? on : stream);
 }
 
-void lsm_ctx::toc(const char *name, hipEvent_t a) {
+void lsm_ctx::toc(const char *name, hipEvent_t a, hipStream_t on) {
     if (!timing || !a) return;
     hipEvent_t b = get_event();
-    (void)hipEventRecord(b, stream);
+    (void)hipEventRecord(b, on ? on : stream);
     pending.push_back({name, a, b});
 }
 
 void lsm_ctx::collect_timings() {
+    std::vector<Pending> later;   // (side-stream brackets still running: the next collection)
     for (auto &pe : pending) {
+        if (hipEventQuery(pe.b) == hipErrorNotReady) {
+            later.push_back(pe);
+            continue;
+        }
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
             KStat &s = stats[pe.name];
@@ -113,12 +119,30 @@ void lsm_ctx::collect_timings() {
         event_pool.push_back(pe.a);
         event_pool.push_back(pe.b);
     }
-    pending.clear();
+    pending.swap(later);
+}
+
+void lsm_ctx::join_side() {
+    if (!side_pending) return;
+    (void)hipStreamSynchronize(side);
+    side_pending = false;
+}
+
+void lsm_ctx::join_side_device() {
+    if (!side_pending) return;
+    (void)hipStreamWaitEvent(stream, side_ev, 0);
+    side_pending = false;
+}
+
+// the entry points' cloud lookup: first the normals' side-stream work completes (join_side)
+static Cloud *find_cloud_nojoin(lsm_ctx *ctx, lsm_cloud id) {
+    auto it = ctx->clouds.find(id);
+    return it == ctx->clouds.end() ? nullptr : it->second;
 }
 
 static Cloud *find_cloud(lsm_ctx *ctx, lsm_cloud id) {
-    auto it = ctx->clouds.find(id);
-    return it == ctx->clouds.end() ? nullptr : it->second;
+    ctx->join_side();
+    return find_cloud_nojoin(ctx, id);
 }
 
 static void free_cloud(Cloud *c) {
@@ -140,7 +164,9 @@ static void free_cloud(Cloud *c) {
 static int complete_normals(lsm_ctx *ctx, Cloud *c) {
     if (!c->lazy) return LSM_OK;
     std::vector<Cloud *> one{c};
-    return lsm_normals_complete(ctx, one);
+    const int rc = lsm_normals_complete(ctx, one);
+    ctx->join_side_device();   // the caller's next work on the stream reads the normals
+    return rc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -196,6 +222,7 @@ int lsm_init(int device, lsm_ctx **out) {
 int lsm_free(lsm_ctx *ctx) {
     if (!ctx) return LSM_EINVAL;
     (void)hipSetDevice(ctx->device);
+    ctx->join_side();
     (void)hipStreamSynchronize(ctx->stream);
     for (auto &kv : ctx->clouds) free_cloud(kv.second);
     for (auto &kv : ctx->scratch) (void)hipFree(kv.second.p);
@@ -206,6 +233,8 @@ int lsm_free(lsm_ctx *ctx) {
     }
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->pinned2) (void)hipHostFree(ctx->pinned2);
+    if (ctx->side_ev) (void)hipEventDestroy(ctx->side_ev);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return LSM_OK;
@@ -661,8 +690,8 @@ int lsm_icp_batch(lsm_ctx *ctx, int64_t npairs, const lsm_cloud *src, const lsm_
     if (rc) return rc;
     std::vector<Cloud *> s(static_cast<size_t>(npairs)), t(static_cast<size_t>(npairs));
     for (int64_t i = 0; i < npairs; ++i) {
-        s[i] = find_cloud(ctx, src[i]);
-        t[i] = find_cloud(ctx, tgt[i]);
+        s[i] = find_cloud_nojoin(ctx, src[i]);   // (the ICP joins the side stream on the
+        t[i] = find_cloud_nojoin(ctx, tgt[i]);   //  device, before its first accumulation)
         if (!s[i] || !t[i]) {
             ctx->set_error("unknown cloud handle");
             return LSM_EINVAL;

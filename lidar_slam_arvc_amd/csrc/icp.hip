@@ -2353,6 +2353,9 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
         ctx->toc("nn_fallback", ev);
         ctx->tic("accumulate", &ev);
+        // the normals' side-stream refine (pre-processing or the lazy targets above) has
+        // overlapped this pass's correspondence search; the accumulation reads the normals
+        ctx->join_side_device();
         if (p.method == LSM_P2PLANE)
             accumulate_kernel<LSM_P2PLANE><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, d_corr,
                                                                         d_part);

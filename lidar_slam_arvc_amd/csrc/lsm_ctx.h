@@ -54,6 +54,15 @@ struct KStat {
 struct lsm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // the normals' refine kernel (a handful of long single-lane scans) runs on `side`, so the
+    // next ICP's first correspondence pass (which reads no normals) overlaps it; side_ev marks its
+    // end. Every entry point but the ICP waits for it (join_side); the ICP waits on the device
+    // before its first accumulation (join_side_device)
+    hipStream_t side = nullptr;
+    hipEvent_t side_ev = nullptr;
+    bool side_pending = false;
+    void join_side();
+    void join_side_device();
     std::string err;
     std::unordered_map<int64_t, Cloud *> clouds;
     int64_t next_id = 1;
@@ -89,8 +98,8 @@ struct lsm_ctx {
     void *pinned2 = nullptr;
     hipEvent_t get_event();
     // bracket a launch with events when timing is on
-    void tic(const char *name, hipEvent_t *a);
-    void toc(const char *name, hipEvent_t a);
+    void tic(const char *name, hipEvent_t *a, hipStream_t on = nullptr);
+    void toc(const char *name, hipEvent_t a, hipStream_t on = nullptr);
     void collect_timings();   // call after the stream is synchronised
 };
 

@@ -1769,14 +1769,27 @@ normals_refine_kernel(const CloudDev *cd, const GridGeo *geo, NormalParams np,
 // The dense half of the split launch: the dense lists' points, then the few the dense kernel
 // deferred to a refine scan. rlist / rcnt: scratch of the dense lists' size / K words.
 template <int G>
-void launch_dense_half(hipStream_t st, const Seg *d_segs, int nseg, const CloudDev *d_cd,
-                       const GridGeo *d_geo, int K, const NormalParams &np, const uint32_t *dlist,
-                       const uint32_t *dcnt, unsigned long long *d_ns, uint32_t *rlist,
-                       uint32_t *rcnt) {
+void launch_dense_half(hipStream_t st, hipStream_t rst, const Seg *d_segs, int nseg,
+                       const CloudDev *d_cd, const GridGeo *d_geo, int K, const NormalParams &np,
+                       const uint32_t *dlist, const uint32_t *dcnt, unsigned long long *d_ns,
+                       uint32_t *rlist, uint32_t *rcnt, lsm_ctx *ctx, const char *stat) {
     normals_dense_kernel<G><<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, d_geo, np, dlist, dcnt,
                                                          d_ns, rlist, rcnt);
-    normals_refine_kernel<G><<<dim3(K, REFINE_BLOCKS), PT_THREADS, 0, st>>>(d_cd, d_geo, np, rlist,
-                                                                           rcnt, d_ns);
+    // the refine scans (a few long single-lane chains) on rst: the side stream when it may
+    // overlap what follows (lsm_ctx::side)
+    // (not timed there: overlapped, its event window would measure the ICP kernels it shares the
+    // chip with; its instructions are 0.2 % of the normals', bench.py leaves them out as well)
+    (void)stat;
+    if (rst != st) {
+        (void)hipEventRecord(ctx->side_ev, st);
+        (void)hipStreamWaitEvent(rst, ctx->side_ev, 0);
+    }
+    normals_refine_kernel<G><<<dim3(K, REFINE_BLOCKS), PT_THREADS, 0, rst>>>(d_cd, d_geo, np, rlist,
+                                                                            rcnt, d_ns);
+    if (rst != st) {
+        (void)hipEventRecord(ctx->side_ev, rst);
+        ctx->side_pending = true;
+    }
 }
 
 #ifdef LSM_DIAG
@@ -2264,9 +2277,11 @@ int normals_phases(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_
 // In statistics mode (lsm_set_timing(ctx, 2)) it also counts the neighbours of every normal
 // (SURVEY.md §8d's algorithmic work) and the points that needed the kNN truncation.
 int run_normals(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
-                const GridGeo *d_geo, int K, size_t N, const NormalParams &np, int64_t npts) {
+                const GridGeo *d_geo, int K, size_t N, const NormalParams &np, int64_t npts,
+                const char *stat) {
     if (nseg <= 0) return LSM_OK;
     hipStream_t st = ctx->stream;
+    ctx->join_side_device();   // an earlier refine may still read the list buffers below
     unsigned long long *d_ns = nullptr;
     if (ctx->statistics) {
         d_ns = (unsigned long long *)ctx->buf("n_stats", 72 * 8);
@@ -2287,8 +2302,21 @@ int run_normals(lsm_ctx *ctx, const Seg *d_segs, int nseg, const CloudDev *d_cd,
         LSM_HIP_TRY(ctx, hipMemsetAsync(dcnt, 0, size_t(K) * 8, st));
         normals_sparse_kernel<NORMALS_G_DEFAULT><<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, d_geo,
                                                                              np, dlist, dcnt, d_ns);
-        launch_dense_half<NORMALS_GD_DEFAULT>(st, d_segs, nseg, d_cd, d_geo, K, np, dlist, dcnt,
-                                              d_ns, rlist, dcnt + K);
+        // LSM_NORMALS_SIDE (default 1): the refine kernel on the side stream (not with the
+        // statistics, which read its counters right away)
+        hipStream_t rst = st;
+        if (!d_ns && lsm_knob("LSM_NORMALS_SIDE", 1.0) != 0.0) {
+            if (!ctx->side) {
+                if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming) != hipSuccess) {
+                    ctx->set_error("side stream creation failed");
+                    return LSM_EHIP;
+                }
+            }
+            rst = ctx->side;
+        }
+        launch_dense_half<NORMALS_GD_DEFAULT>(st, rst, d_segs, nseg, d_cd, d_geo, K, np, dlist,
+                                              dcnt, d_ns, rlist, dcnt + K, ctx, stat);
     } else {
         normals_kernel<NORMALS_G_DEFAULT><<<nseg, PT_THREADS, 0, st>>>(d_segs, d_cd, np, d_ns);
     }
@@ -2469,7 +2497,9 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         int64_t npts = 0;
         for (int k = 0; k < K; ++k) npts += wn[k];
         ctx->tic("normals", &ev);
-        if ((rc = run_normals(ctx, d_psegs, int(psegs.size()), d_cd, d_geo, K, N, np, npts))) return rc;
+        if ((rc = run_normals(ctx, d_psegs, int(psegs.size()), d_cd, d_geo, K, N, np, npts,
+                              "normals")))
+            return rc;
         ctx->toc("normals", ev);
     }
 
@@ -2529,7 +2559,8 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
         hipEvent_t ev;
         ctx->tic("normals_lazy", &ev);
         if ((rc = run_normals(ctx, d_segs, int(segs.size()), d_cd, d_gg, int(grp.size()),
-                              std::max<size_t>(tot, 1), normal_params(r, mnn), int64_t(tot))))
+                              std::max<size_t>(tot, 1), normal_params(r, mnn), int64_t(tot),
+                              "normals_lazy")))
             return rc;
         ctx->toc("normals_lazy", ev);
         LSM_HIP_TRY(ctx, hipStreamSynchronize(st));

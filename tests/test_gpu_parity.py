@@ -148,7 +148,8 @@ def test_normals_preclassification_bit_identical(dev, seq64k, max_nn, monkeypatc
 def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
     """The split launch (default: the points predicted sparse, then every deferred point in
     full waves of the clouds' dense lists, then the rare refine scans) against the one-kernel
-    launch (LSM_NORMALS_SPLIT=0):
+    launch (LSM_NORMALS_SPLIT=0) and against the split launch with its refine kernel on the main
+    stream instead of the side stream (LSM_NORMALS_SIDE=0):
     bit-identical normals on bench scans, under heavier truncation, on degenerate neighbourhoods
     (duplicates saturating a u8 bin, a dense patch) and on clouds that carry prior normals
     (EstimateNormals re-run on a cloud with normals orients to them)."""
@@ -161,8 +162,10 @@ def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
     keep = _lib.prep_params(max_nn=max_nn, min_radius=-np.inf, max_radius=1e15,
                             min_height=-1e15, max_height=1e15)
     out = {}
-    for split in ("1", "0"):
-        monkeypatch.setenv("LSM_NORMALS_SPLIT", split)
+    for split in ("1", "0", "side0"):
+        # "side0": the split launch with its refine kernel on the main stream (LSM_NORMALS_SIDE=0)
+        monkeypatch.setenv("LSM_NORMALS_SPLIT", "1" if split == "side0" else split)
+        monkeypatch.setenv("LSM_NORMALS_SIDE", "0" if split == "side0" else "1")
         ids = [dev.upload(c) for c in clouds]
         try:
             dev.preprocess(ids, prm)
@@ -173,8 +176,9 @@ def test_normals_split_launch_bit_identical(dev, seq64k, max_nn, monkeypatch):
         finally:
             _release(dev, ids)
     monkeypatch.delenv("LSM_NORMALS_SPLIT")
-    for a, b in zip(out["1"], out["0"]):
-        assert np.array_equal(a, b)
+    monkeypatch.delenv("LSM_NORMALS_SIDE")
+    for a, b, c in zip(out["1"], out["0"], out["side0"]):
+        assert np.array_equal(a, b) and np.array_equal(a, c)
 
 
 @pytest.mark.parametrize("voxel", [0.0, 0.1])
