@@ -96,6 +96,9 @@ struct lsm_ctx {
     void *host_pinned(size_t bytes);
     void *host_pinned_extra(size_t bytes);   // a second, fixed 4 KiB pinned area
     void *pinned2 = nullptr;
+    // grow-only host tables (the launches' workgroup -> (cloud, first point) lists), kept so a
+    // call does not fault in a fresh multi-MB vector (≈ 10 ms of host time per C3 step)
+    std::map<std::string, std::vector<uint64_t>> host_tables;
     hipEvent_t get_event();
     // bracket a launch with events when timing is on
     void tic(const char *name, hipEvent_t *a, hipStream_t on = nullptr);

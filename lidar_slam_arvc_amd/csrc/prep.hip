@@ -1865,6 +1865,17 @@ download_kernel(const float4 *xyz, const float4 *nrm, const uint32_t *perm, int 
 }
 
 // helpers ----------------------------------------------------------------------------------
+// A launch's workgroup table: (cloud, first point) per per_block points of every cloud, in the
+// context's grow-only host storage (a fresh vector per call cost page faults)
+struct SegTable {
+    const Seg *p = nullptr;
+    size_t n = 0;
+    const Seg *data() const { return p; }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+};
+static_assert(sizeof(Seg) == sizeof(uint64_t), "Seg tables live in u64 storage");
+
 template <typename T>
 int upload_vec(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out) {
     T *d = static_cast<T *>(ctx->buf(name, v.size() * sizeof(T)));
@@ -1874,6 +1885,19 @@ int upload_vec(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out)
     }
     if (!v.empty())
         LSM_HIP_TRY(ctx, hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice,
+                                        ctx->stream));
+    *out = d;
+    return LSM_OK;
+}
+
+int upload_vec(lsm_ctx *ctx, const char *name, const SegTable &v, Seg **out) {
+    Seg *d = static_cast<Seg *>(ctx->buf(name, v.size() * sizeof(Seg)));
+    if (!d) {
+        ctx->set_error(std::string("scratch allocation failed: ") + name);
+        return LSM_ENOMEM;
+    }
+    if (!v.empty())
+        LSM_HIP_TRY(ctx, hipMemcpyAsync(d, v.data(), v.size() * sizeof(Seg), hipMemcpyHostToDevice,
                                         ctx->stream));
     *out = d;
     return LSM_OK;
@@ -1941,11 +1965,17 @@ template <typename Key> using SortConfig = typename SortConfigFor<Key>::type;
 // ==========================================================================================
 namespace {
 
-std::vector<Seg> point_segments(const std::vector<uint32_t> &n, int per_block) {
-    std::vector<Seg> segs;
+SegTable point_segments(lsm_ctx *ctx, const char *name, const std::vector<uint32_t> &n,
+                        int per_block) {
+    size_t tot = 0;
+    for (uint32_t v : n) tot += (size_t(v) + per_block - 1) / size_t(per_block);
+    std::vector<uint64_t> &h = ctx->host_tables[name];
+    if (h.size() < tot) h.resize(tot + tot / 4);
+    Seg *segs = reinterpret_cast<Seg *>(h.data());
+    size_t j = 0;
     for (size_t k = 0; k < n.size(); ++k)
-        for (uint32_t s = 0; s < n[k]; s += per_block) segs.push_back({int32_t(k), int32_t(s)});
-    return segs;
+        for (uint32_t s = 0; s < n[k]; s += uint32_t(per_block)) segs[j++] = {int32_t(k), int32_t(s)};
+    return SegTable{segs, tot};
 }
 
 // filter_radius_height over the batch: writes the kept points of cloud k, in reference order, to
@@ -1959,21 +1989,23 @@ int run_filter(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_params
     const int K = int(clouds.size());
     std::vector<const float *> raw(K);
     std::vector<int32_t> nraw(K), first_block(K), nblocks(K);
-    std::vector<Seg> fsegs;
+    std::vector<uint32_t> nr(K);
     int64_t total_raw = 0;
+    int32_t nb_acc = 0;
     for (int k = 0; k < K; ++k) {
         raw[k] = clouds[k]->d_raw;
         nraw[k] = int32_t(clouds[k]->n_raw);
-        first_block[k] = int32_t(fsegs.size());
-        for (int64_t s = 0; s < clouds[k]->n_raw; s += FILTER_CHUNK)
-            fsegs.push_back({k, int32_t(s)});
-        nblocks[k] = int32_t(fsegs.size()) - first_block[k];
+        first_block[k] = nb_acc;
+        nblocks[k] = int32_t((clouds[k]->n_raw + FILTER_CHUNK - 1) / FILTER_CHUNK);
+        nb_acc += nblocks[k];
         total_raw += clouds[k]->n_raw;
     }
     if (total_raw >= (int64_t(1) << 32)) {
         ctx->set_error("batch too large (>= 2^32 raw points); split the batch");
         return LSM_EINVAL;
     }
+    for (int k = 0; k < K; ++k) nr[k] = uint32_t(clouds[k]->n_raw);
+    const SegTable fsegs = point_segments(ctx, "h_fsegs", nr, FILTER_CHUNK);
     const int nfb = int(fsegs.size());
     int rc;
     const float **d_raw;
@@ -2096,7 +2128,7 @@ int run_voxel(lsm_ctx *ctx, std::vector<Cloud *> &clouds, double v, float4 **pts
     }
     VoxGeo *d_geo;
     if ((rc = upload_vec(ctx, "v_geo", geo, &d_geo))) return rc;
-    std::vector<Seg> segs = point_segments(cnt, PT_THREADS);
+    const SegTable segs = point_segments(ctx, "h_vsegs", cnt, PT_THREADS);
     Seg *d_segs;
     if ((rc = upload_vec(ctx, "v_segs", segs, &d_segs))) return rc;
     const size_t N = std::max<uint32_t>(ntot, 1);
@@ -2452,7 +2484,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     if ((rc = upload_vec(ctx, "g_cd", cdev, &d_cd))) return rc;
     if ((rc = upload_vec(ctx, "g_perm", perm_ptrs, &d_perm_ptrs))) return rc;
     if ((rc = upload_vec(ctx, "g_cellp", cell_ptrs, &d_cell_ptrs))) return rc;
-    std::vector<Seg> psegs = point_segments(wn, PT_THREADS);
+    const SegTable psegs = point_segments(ctx, "h_gsegs", wn, PT_THREADS);
     Seg *d_psegs;
     if ((rc = upload_vec(ctx, "g_segs", psegs, &d_psegs))) return rc;
     uint32_t ntot = 0;
@@ -2549,7 +2581,7 @@ int lsm_normals_complete(lsm_ctx *ctx, std::vector<Cloud *> &clouds) {
             gg[k].n = n[k];
             tot += n[k];
         }
-        std::vector<Seg> segs = point_segments(n, PT_THREADS);
+        const SegTable segs = point_segments(ctx, "h_lzsegs", n, PT_THREADS);
         CloudDev *d_cd;
         Seg *d_segs;
         GridGeo *d_gg;
@@ -2807,7 +2839,8 @@ int lsm_fpfh_run(lsm_ctx *ctx, Cloud *c, double radius, int max_nn) {
     CloudDev *d_cd;
     int rc;
     if ((rc = upload_vec(ctx, "fp_cd", cdv, &d_cd))) return rc;
-    std::vector<Seg> segs = point_segments(std::vector<uint32_t>(1, uint32_t(n)), PT_THREADS);
+    const SegTable segs =
+        point_segments(ctx, "h_fpsegs", std::vector<uint32_t>(1, uint32_t(n)), PT_THREADS);
     Seg *d_segs;
     if ((rc = upload_vec(ctx, "fp_segs", segs, &d_segs))) return rc;
     NormalParams np;
