@@ -41,8 +41,8 @@ VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 2   # = 1228.8
 # measured with 8 waves per SIMD and 8 independent chains (v_fma_f32 in the same kernel: 868 G/s;
 # tools/calib/valu_calib.hip, profiles/r05h/valu_calib.log)
 VALU_F64_PEAK_G = 500.0
-KERNELS = ["filter", "grid", "normals", "normals_lazy", "nn", "nn_fallback", "accumulate",
-           "solve", "voxel"]
+KERNELS = ["filter", "grid", "normals", "normals_lazy", "normals_refine", "nn", "nn_fallback",
+           "accumulate", "solve", "voxel"]
 
 
 def source_sha() -> str:
@@ -148,6 +148,9 @@ def parse():
                     help="0: every core this process may use (affinity mask, capped by the "
                          "cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--save-gathered", default="",
+                    help="loop_closure (C4): rank 0 writes the last step's gathered transforms of "
+                         "all ranks' pairs (global order) to this .npz")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearse the multi-rank path on one GPU: all ranks on device 0, gloo "
                          "collectives on host tensors (tests only; not a scaling measurement)")
@@ -407,6 +410,7 @@ def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda
     wn_mode = ("lazy" if normals == "lazy" else True) if want_normals else False
     ms = None
     S = 1
+    gathered = [None]   # loop_closure: every rank's pair results of the last step, global order
     if ouster:
         from lidar_slam_arvc_amd.multiscale import MultiScaleSet
         ms = MultiScaleSet(dev, ids)                 # per-scale device clones, made once
@@ -430,8 +434,10 @@ def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda
             res = dev.icp_batch_arrays(ids[P:], ids[:P], seq.priors, icp)
             rel = res["transformation"]
             if group is not None:   # the sequence-level exchange: gather every pair's result
-                gather_pair_results(rel, np.arange(first, first + P), world * P, group=group,
-                                    device=cuda)
+                gathered[0] = gather_pair_results(rel, np.arange(first, first + P), world * P,
+                                                  group=group, device=cuda)
+            else:
+                gathered[0] = rel
             return n, res
     else:
         prep = _lib.prep_params(want_normals=wn_mode, grid_cell=grid_cell)
@@ -569,6 +575,10 @@ def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda
                                                   "(profiles/r05h/valu_calib.log)"}
                                        if t_peak else None),
                       "ms_per_step": round(step_s * 1e3, 4),
+                      # the refine kernel's own window on the side stream (it overlaps the ICP's
+                      # first correspondence pass, so it is not part of ms_per_step)
+                      "refine_ms_per_step_overlapped": round(stats["normals_refine"]["ms"] /
+                                                             args.steps, 4),
                       "launches_per_step": (stats["normals"]["launches"] +
                                             stats["normals_lazy"]["launches"]) / args.steps,
                       "flops": {"unit": "TFLOP/s", "achieved": round(flops / step_s / 1e12, 4),
@@ -593,6 +603,11 @@ def run_workload(workload, seq, P, args, *, gpu, local, rank, world, group, cuda
 
     n_pts, res = last
     iters = list(res["iterations"])
+    if loop and rank == 0 and args.save_gathered:
+        # the gathered transforms of all world x P pairs (tools/c4_gather_check.py compares them
+        # with one context registering every pair in one batch)
+        np.savez_compressed(args.save_gathered, transformation=gathered[0], world=world,
+                            pairs_per_rank=P, seed=args.seed if args.seed >= 0 else 4)
     if rank != 0:
         return None
     achieved = nn["algo_bytes"] / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0

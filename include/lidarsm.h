@@ -226,7 +226,9 @@ int lsm_se3_prefix(const double *rel, int64_t n, double *out);
  *   "normals"                          estimate_normals in the pre-process (the split launch)
  *   "normals_lazy"                     LSM_NORMALS_LAZY clouds' normals, computed by a P2Plane
  *                                      registration or another first use
- *   "nn", "nn_fallback"                the correspondence search and its fallback, per pass
+ *   "normals_refine"                   the normals' refine kernel (both of the above), timed on
+ *                                      the side stream it runs on, overlapping the next ICP
+ *   "nn", "nn_fallback"               the correspondence search and its fallback, per pass
  *   "accumulate", "solve"              the JtJ / moment sums and the per-pair solve, per pass
  *   "plane", "ransac", "fpfh", "feature_nn"   icp2planes and fpfh
  * Aggregates: "nn_pass" (launches = correspondence passes; ms = "nn" + "nn_fallback" of those

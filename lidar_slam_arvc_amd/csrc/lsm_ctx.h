@@ -57,7 +57,11 @@ struct lsm_ctx {
     // the normals' refine kernel (a handful of long single-lane scans) runs on `side`, so the
     // next ICP's first correspondence pass (which reads no normals) overlaps it; side_ev marks its
     // end. Every entry point but the ICP waits for it (join_side); the ICP waits on the device
-    // before its first accumulation (join_side_device)
+    // before its first accumulation (join_side_device).
+    // Invariant: the refine reads its launch's CloudDev / GridGeo tables and the normals' list
+    // buffers; every writer of those (prep.hip's upload_vec, run_normals) joins first. A new entry
+    // point that writes them without going through find_cloud (a host join) or upload_vec must
+    // call join_side_device() before its first write.
     hipStream_t side = nullptr;
     hipEvent_t side_ev = nullptr;
     bool side_pending = false;

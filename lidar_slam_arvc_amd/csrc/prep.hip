@@ -1777,15 +1777,18 @@ void launch_dense_half(hipStream_t st, hipStream_t rst, const Seg *d_segs, int n
                                                          d_ns, rlist, rcnt);
     // the refine scans (a few long single-lane chains) on rst: the side stream when it may
     // overlap what follows (lsm_ctx::side)
-    // (not timed there: overlapped, its event window would measure the ICP kernels it shares the
-    // chip with; its instructions are 0.2 % of the normals', bench.py leaves them out as well)
+    // Timed under its own name ("normals_refine"): on the side stream its window overlaps the
+    // ICP kernels it shares the chip with, so it is reported beside the normals' time, not in it.
     (void)stat;
     if (rst != st) {
         (void)hipEventRecord(ctx->side_ev, st);
         (void)hipStreamWaitEvent(rst, ctx->side_ev, 0);
     }
+    hipEvent_t ev;
+    ctx->tic("normals_refine", &ev, rst);
     normals_refine_kernel<G><<<dim3(K, REFINE_BLOCKS), PT_THREADS, 0, rst>>>(d_cd, d_geo, np, rlist,
                                                                             rcnt, d_ns);
+    ctx->toc("normals_refine", ev, rst);
     if (rst != st) {
         (void)hipEventRecord(ctx->side_ev, rst);
         ctx->side_pending = true;
@@ -1876,8 +1879,14 @@ struct SegTable {
 };
 static_assert(sizeof(Seg) == sizeof(uint64_t), "Seg tables live in u64 storage");
 
+// Every table upload of the pre-processing and normals paths first orders the main stream after
+// a refine kernel still running on the side stream (lsm_ctx::side): the refine reads the launch's
+// CloudDev / GridGeo tables (g_cd / g_geo, lz_cd / lz_gg), and the next upload may overwrite them
+// before run_normals' own join (lsm_normals_complete's (radius, max_nn) groups did). The join is a
+// device-side wait, only recorded while a refine is pending.
 template <typename T>
 int upload_vec(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out) {
+    ctx->join_side_device();
     T *d = static_cast<T *>(ctx->buf(name, v.size() * sizeof(T)));
     if (!d) {
         ctx->set_error(std::string("scratch allocation failed: ") + name);
@@ -1891,6 +1900,7 @@ int upload_vec(lsm_ctx *ctx, const char *name, const std::vector<T> &v, T **out)
 }
 
 int upload_vec(lsm_ctx *ctx, const char *name, const SegTable &v, Seg **out) {
+    ctx->join_side_device();
     Seg *d = static_cast<Seg *>(ctx->buf(name, v.size() * sizeof(Seg)));
     if (!d) {
         ctx->set_error(std::string("scratch allocation failed: ") + name);

@@ -663,6 +663,30 @@ def test_lazy_normals_revisit_pairs_and_p2p(dev):
         _release(dev, eager + lazy)
 
 
+def test_lazy_normals_mixed_radii_in_one_batch(dev):
+    """One P2Plane batch whose lazy targets were pre-processed with different normal parameters
+    (three (radius, max_nn) groups: lsm_normals_complete runs one normals launch per group, each
+    with a refine kernel on the side stream that reads the group's tables while the next group
+    uploads its own): registrations and completed normals equal the eager clouds'."""
+    seq = synthetic.make_sequence(7, seed=3, model=synthetic.HDL64)
+    groups = [dict(normal_radius=0.3, max_nn=300), dict(normal_radius=0.5, max_nn=30),
+              dict(normal_radius=0.2, max_nn=300)]
+    icp = _lib.icp_params()
+    eager, lazy = [], []
+    try:
+        for k, s in enumerate(seq.scans):
+            kw = groups[k % 3]
+            eager += _prep(dev, [s], **kw)
+            lazy += _prep(dev, [s], want_normals="lazy", **kw)
+        ref = dev.icp_batch_arrays(eager[1:], eager[:-1], seq.priors, icp)
+        got = dev.icp_batch_arrays(lazy[1:], lazy[:-1], seq.priors, icp)
+        _assert_batch_equal(ref, got)
+        for e, l in zip(eager, lazy):
+            assert np.array_equal(dev.download(e, normals=True)[1], dev.download(l, normals=True)[1])
+    finally:
+        _release(dev, eager + lazy)
+
+
 def test_lazy_normals_completed_for_other_uses(dev, seq64k):
     """Every other use of the normals (FPFH, the plane split's priors, voxel_down_sample with
     normals, download) completes the pending ones first: the same results as eager clouds."""

@@ -266,6 +266,14 @@ def compare(gpu, cpu) -> dict:
                        "rmse_cpu": float(cpu["inlier_rmse"][k])} for k in nonconv],
         },
         "outside_tolerance_converged": [int(k) for k in np.flatnonzero(conv & ~inside)],
+        # every pair outside the bar, itemised (both sides' iterations, fitness and rmse)
+        "outside_tolerance": [{"pair": int(k), "dR": float(dR[k]), "dt_m": float(dt[k]),
+                               "iters_gpu": int(ig[k]), "iters_cpu": int(ic[k]),
+                               "fitness_gpu": float(gpu["fitness"][k]),
+                               "fitness_cpu": float(cpu["fitness"][k]),
+                               "rmse_gpu": float(gpu["inlier_rmse"][k]),
+                               "rmse_cpu": float(cpu["inlier_rmse"][k])}
+                              for k in np.flatnonzero(~inside)],
     }
 
 
@@ -282,7 +290,8 @@ def compare_workload(gpu, cpu, workload: str) -> dict:
         {k: np.asarray(gpu[k])[s] for k in keys},
         {k: np.asarray(cpu[k])[s] for k in keys}).items()
         if k in ("pairs", "within_tolerance", "converged_both", "iterations_equal",
-                 "worst_converged", "outside_tolerance_converged")}} for s in range(S)]
+                 "worst_converged", "outside_tolerance_converged",
+                 "outside_tolerance")}} for s in range(S)]
     return out
 
 

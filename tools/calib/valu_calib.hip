@@ -69,6 +69,26 @@ __global__ void __launch_bounds__(256) issue_add64(double *out, double a, double
     out[blockIdx.x * 256 + threadIdx.x] = r0 + r1 + r2 + r3 + r4 + r5 + r6 + r7;
 }
 
+// (3) f64 MFMA throughput (could the normals' f64 cumulant sums run as
+//     v_mfma_f64_16x16x4f64 tiles?): 8 independent accumulators per wave, 8 waves per SIMD.
+typedef double d4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) mfma64(double *out, double a, double b) {
+    d4 c0 = {a, b, a, b}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0, c7 = c0;
+    const double x = a + threadIdx.x * 1e-9, y = b - threadIdx.x * 1e-9;
+    for (int i = 0; i < M; ++i) {
+        c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c3, 0, 0, 0);
+        c4 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c4, 0, 0, 0);
+        c5 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c5, 0, 0, 0);
+        c6 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c6, 0, 0, 0);
+        c7 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c7, 0, 0, 0);
+    }
+    const d4 s = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
+    out[blockIdx.x * 256 + threadIdx.x] = s.x + s.y + s.z + s.w;
+}
+
 template <typename K, typename T>
 float timed(K k, T *o, T a, T b, int blocks) {
     hipEvent_t e0, e1;
@@ -100,6 +120,13 @@ int main() {
     printf("issue v_fma_f64 x8: %.3f ms, %.1f G wave-instr/s\n", ms, waves * (M * 8.0) / ms / 1e6);
     ms = timed(issue_add64, o64, 0.999, 0.001, blocks);
     printf("issue v_add_f64 x8: %.3f ms, %.1f G wave-instr/s\n", ms, waves * (M * 8.0) / ms / 1e6);
+    ms = timed(mfma64, o64, 0.999, 0.001, blocks);
+    {
+        const double inst = waves * (M * 8.0);
+        printf("mfma v_mfma_f64_16x16x4f64 x8: %.3f ms, %.2f G wave-instr/s, %.1f TFLOP/s "
+               "(2048 FLOP each), %.1f cycles/SIMD each at 2.4 GHz\n", ms, inst / ms / 1e6,
+               inst * 2048.0 / ms / 1e9, 1024.0 * 2.4e9 / (inst / (ms * 1e-3)));
+    }
     printf("(peak assumed by bench.py: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles = 1228.8 G/s)\n");
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
