@@ -37,8 +37,9 @@ F32_CYC = 1024 * 2.4e9 / 868e9      # 2.83
 F64_CYC = 1024 * 2.4e9 / 500e9      # 4.92
 
 
-def final_windows(g, q, rad):
-    """Per query: list of (lo, hi) index ranges into g.key of its final-pass row windows."""
+def final_windows(g, q, rad, with_rows=False):
+    """Per query: list of (lo, hi) index ranges into g.key of its final-pass row windows
+    (with_rows: (row, lo, hi))."""
     qx, qy, qz = q[:, 0] - g.o[0], q[:, 1] - g.o[1], q[:, 2] - g.o[2]
     prune = rad * 1.0001 + 1e-6
     cy, cz = np.floor(qy / g.py).astype(np.int64), np.floor(qz / g.pz).astype(np.int64)
@@ -57,9 +58,22 @@ def final_windows(g, q, rad):
             ch = np.sqrt(np.maximum(prune ** 2 - dyz2, 0.0))
             a = np.searchsorted(g.key, row + qx - ch, "left")
             b = np.searchsorted(g.key, row + qx + ch, "right")
+            rid = (iz * g.ny + iy)
             for k in np.flatnonzero(ok & (b > a)):
-                out[k].append((int(a[k]), int(b[k])))
+                out[k].append((int(rid[k]), int(a[k]), int(b[k])) if with_rows else
+                              (int(a[k]), int(b[k])))
     return out
+
+
+def hull_len(wins):
+    """Candidates of a group that walks, per row any of its queries touches, one window from the
+    smallest left end to the largest right end (what a wave can enumerate cheaply)."""
+    rows = {}
+    for w in wins:
+        for r, a, b in w:
+            lo, hi = rows.get(r, (a, b))
+            rows[r] = (min(lo, a), max(hi, b))
+    return sum(hi - lo for lo, hi in rows.values())
 
 
 def union_len(ranges):
@@ -91,7 +105,8 @@ def model_scan(pts, mfma_cyc):
     top = np.minimum(np.floor(d300 ** 2 * PM.NB8 / PM.R ** 2) + 1, PM.NB8) * PM.R ** 2 / PM.NB8
     rad = np.sqrt(top)
     g = PM.AnisoGrid(pts, 0.375, 0.375)
-    win = final_windows(g, q, rad)
+    winr = final_windows(g, q, rad, with_rows=True)
+    win = [[(a, b) for _, a, b in w] for w in winr]
     steps = np.array([sum(b - a for a, b in w) for w in win], np.float64)
     members = np.array([len(tree.query_ball_point(p, r * 0.99999)) for p, r in zip(q, rad)],
                        np.float64)
@@ -109,10 +124,12 @@ def model_scan(pts, mfma_cyc):
     Q = 16
     uni = np.array([union_len([r for w in win[i:i + Q] for r in w]) for i in range(0, n, Q)],
                    np.float64)
+    hull = np.array([hull_len(winr[i:i + Q]) for i in range(0, n, Q)], np.float64)
     gsz = np.array([len(win[i:i + Q]) for i in range(0, n, Q)], np.float64)
     mstep_valu = 11 * F32_CYC + 3 * F64_CYC
     mfma_steps = np.ceil(uni / 4.0)
     mfma_cyc_total = float((mfma_steps * max(mfma_cyc, mstep_valu)).sum() / n)
+    hull_cyc_total = float((np.ceil(hull / 4.0) * max(mfma_cyc, mstep_valu)).sum() / n)
     mean_win = float(steps.mean())
     return {
         "dense_points": int(n),
@@ -122,9 +139,12 @@ def model_scan(pts, mfma_cyc):
         # candidates a group tests per query, over the candidates a lane walks for its own query
         "union_overhead_16": float(uni.sum() / (steps.sum() / Q)),
         "union_candidates_per_group_mean": float(uni.mean()),
+        "row_hull_overhead_16": float(hull.sum() / (steps.sum() / Q)),
         "issue_cycles_per_dense_point": {"per_lane_f64_valu": lane_cyc,
-                                         "mfma_f64_16x16x4": mfma_cyc_total},
+                                         "mfma_f64_16x16x4": mfma_cyc_total,
+                                         "mfma_f64_16x16x4_row_hull": hull_cyc_total},
         "mfma_over_per_lane": mfma_cyc_total / lane_cyc,
+        "mfma_row_hull_over_per_lane": hull_cyc_total / lane_cyc,
         "group_sizes": float(gsz.mean()),
     }
 
@@ -147,7 +167,8 @@ def main():
         per.append(r)
     summ = {k: float(np.mean([p[k] for p in per])) for k in
             ("final_window_mean", "final_members_mean", "per_lane_wave_divergence",
-             "union_overhead_16", "mfma_over_per_lane")}
+             "union_overhead_16", "row_hull_overhead_16", "mfma_over_per_lane",
+             "mfma_row_hull_over_per_lane")}
     summ["issue_cycles_per_dense_point"] = {
         k: float(np.mean([p["issue_cycles_per_dense_point"][k] for p in per]))
         for k in per[0]["issue_cycles_per_dense_point"]}
