@@ -133,11 +133,6 @@ int lsm_cloud_voxel_keys(lsm_ctx *ctx, lsm_cloud cloud, int32_t *keys, int64_t c
  * receives the number of cells. The tests compare the grid builds with it. */
 int lsm_cloud_layout(lsm_ctx *ctx, lsm_cloud cloud, int32_t *perm, int64_t cap, uint32_t *cells,
                      int64_t cell_cap, int64_t *ncells);
-/* Diagnostics (no reference counterpart): the row occupancy words of a processed cloud's grid
- * (one 64-bit word per row of a layout block, bit x set when cell x of the row holds points; the
- * walks skip empty rows with them). words may be NULL; *nwords receives the count. */
-int lsm_cloud_row_occupancy(lsm_ctx *ctx, lsm_cloud cloud, uint64_t *words, int64_t cap,
-                            int64_t *nwords);
 
 /* Registration (KeyFrame.local_registration_simple, keyframe.py:231-260) --------------------
  * src = `other` (keyframe j), tgt = `self` (keyframe i); the result maps src into tgt frame. */

@@ -24,7 +24,7 @@ EXPORTED = [
     "lsm_init", "lsm_free", "lsm_last_error", "lsm_version", "lsm_default_prep_params",
     "lsm_default_icp_params", "lsm_cloud_upload", "lsm_cloud_upload_f64", "lsm_cloud_clone", "lsm_cloud_release",
     "lsm_cloud_info", "lsm_preprocess", "lsm_preprocess_batch", "lsm_cloud_download",
-    "lsm_cloud_voxel_keys", "lsm_cloud_layout", "lsm_cloud_row_occupancy", "lsm_icp", "lsm_icp_batch", "lsm_icp_last_correspondences",
+    "lsm_cloud_voxel_keys", "lsm_cloud_layout", "lsm_icp", "lsm_icp_batch", "lsm_icp_last_correspondences",
     "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
     "lsm_reset_stats", "lsm_ground_plane", "lsm_plane_samples_get", "lsm_split_plane",
     "lsm_fpfh", "lsm_fpfh_download", "lsm_feature_correspondences", "lsm_ransac_feature",
@@ -82,8 +82,6 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "lsm_cloud_voxel_keys": (C.c_int, [_P, C.c_int64, _i32p, C.c_int64]),
         "lsm_cloud_layout": (C.c_int, [_P, C.c_int64, _i32p, C.c_int64, C.POINTER(C.c_uint32),
                                        C.c_int64, _i64p]),
-        "lsm_cloud_row_occupancy": (C.c_int, [_P, C.c_int64, C.POINTER(C.c_uint64), C.c_int64,
-                                              _i64p]),
         "lsm_icp": (C.c_int, [_P, C.c_int64, C.c_int64, _f64p, C.POINTER(IcpParams),
                               C.POINTER(IcpResult)]),
         "lsm_icp_batch": (C.c_int, [_P, C.c_int64, _i64p, _i64p, _f64p, C.POINTER(IcpParams),
@@ -324,17 +322,6 @@ class Device:
                                              _ptr(cells, C.c_uint32), cells.size,
                                              _ptr(nc, C.c_int64)), "lsm_cloud_layout")
         return perm, cells
-
-    def row_occupancy(self, cloud: int) -> np.ndarray:
-        """The grid's row occupancy words (diagnostics: lsm_cloud_row_occupancy)."""
-        nw = np.zeros(1, dtype=np.int64)
-        self.check(self.lib.lsm_cloud_row_occupancy(self.handle, int(cloud), None, 0,
-                                                    _ptr(nw, C.c_int64)), "lsm_cloud_row_occupancy")
-        w = np.empty(int(nw[0]), dtype=np.uint64)
-        self.check(self.lib.lsm_cloud_row_occupancy(self.handle, int(cloud), _ptr(w, C.c_uint64),
-                                                    w.size, _ptr(nw, C.c_int64)),
-                   "lsm_cloud_row_occupancy")
-        return w
 
     # -- registration ------------------------------------------------------------------------
     def icp_batch(self, src, tgt, init, params: IcpParams):

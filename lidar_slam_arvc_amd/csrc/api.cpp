@@ -22,7 +22,7 @@ static const char *kVersion = "liblidarsm 0.1 (gfx950)";
 static const char *const kKnobs[] = {
     "LSM_NN_SPLIT",  "LSM_NN_SPLIT_PLACE", "LSM_NN_NOCERT", "LSM_NN_CERT_FROM",  "LSM_NN_DIRECT",
     "LSM_NN_DIRECT_ITER", "LSM_NN_KCOLD", "LSM_NN_KMAX",   "LSM_NN_COLD_SEED",  "LSM_NORMALS_EXACT",
-    "LSM_NORMALS_SPLIT", "LSM_NORMALS_SIDE", "LSM_NN_TILE", "LSM_NN_FULL_L", "LSM_FB_GL", "LSM_FB_WAVES", "LSM_FB_WIDE_FROM", "LSM_FB_FAR", "LSM_FB_WIDE_MAX", "LSM_FB_WIDE_MAXC", "LSM_FUSE_ACC"};
+    "LSM_NORMALS_SPLIT", "LSM_NORMALS_SIDE", "LSM_NN_TILE", "LSM_NN_FULL_L", "LSM_FB_GL", "LSM_FB_WAVES", "LSM_FB_WIDE_FROM", "LSM_FB_FAR", "LSM_FB_WIDE_MAX", "LSM_FB_WIDE_MAXC"};
 
 double lsm_knob(const char *name, double dflt) {
     bool known = false;
@@ -152,7 +152,6 @@ static void free_cloud(Cloud *c) {
     (void)hipFree(c->d_perm);
     (void)hipFree(c->d_cell);
     (void)hipFree(c->d_bmask);
-    (void)hipFree(c->d_rocc);
     (void)hipFree(c->d_vox);
     (void)hipFree(c->d_vkeys);
     (void)hipFree(c->d_prior_ref);
@@ -663,34 +662,6 @@ int lsm_cloud_layout(lsm_ctx *ctx, lsm_cloud cloud, int32_t *perm, int64_t cap, 
     if (cells)
         LSM_HIP_TRY(ctx, hipMemcpyAsync(cells, c->d_cell, size_t(nc + 1) * 4,
                                         hipMemcpyDeviceToHost, ctx->stream));
-    LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return LSM_OK;
-}
-
-int lsm_cloud_row_occupancy(lsm_ctx *ctx, lsm_cloud cloud, uint64_t *words, int64_t cap,
-                            int64_t *nwords) {
-    if (!ctx || !nwords) return LSM_EINVAL;
-    Cloud *c = find_cloud(ctx, cloud);
-    if (!c) {
-        ctx->set_error("unknown cloud handle");
-        return LSM_EINVAL;
-    }
-    if (!c->processed) {
-        ctx->set_error("cloud is not processed");
-        return LSM_ESTATE;
-    }
-    const int64_t nw = (int64_t(c->dev.nbx) * c->dev.nby * c->dev.nbz * LSM_BLK_CELLS) >>
-                       LSM_BLKX_SHIFT;
-    *nwords = nw;
-    if (!words) return LSM_OK;
-    if (cap < nw) {
-        ctx->set_error("row occupancy capacity too small");
-        return LSM_EINVAL;
-    }
-    (void)hipSetDevice(ctx->device);
-    if (nw > 0)
-        LSM_HIP_TRY(ctx, hipMemcpyAsync(words, c->d_rocc, size_t(nw) * 8, hipMemcpyDeviceToHost,
-                                        ctx->stream));
     LSM_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return LSM_OK;
 }

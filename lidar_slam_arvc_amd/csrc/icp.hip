@@ -642,26 +642,12 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
             // The row's block parts left to right. (Centre-out with the far parts pruned by
             // their x-slab -- fewer entry searches in the cold pass 0 -- measured slower: nn
             // 81.7 -> 91.3 ms per step, 88.5 with the registers capped back to 7 waves/SIMD.)
-            // Empty row parts end at their occupancy word (a block's 16 rows share one 128-B
-            // line; 2 of 3 row parts a search visits are empty), occupied ones narrow to their
-            // first and last occupied cell -- the same point run -- before the cell table
             int x = xa;
             while (x <= xb) {
                 const int xe = min(xb, x | (LSM_BLKX - 1));   // end of this block's row part
-#if LSM_ROCC
-                const uint64_t ob = lsm_row_bits(G.rocc, G.nbx, G.nby, x, xe, y, z);
-                if (ob) {
-                    const int xb0 = x & ~(LSM_BLKX - 1);
-                    const int fa = xb0 + __builtin_ctzll(ob), fb = xb0 + 63 - __builtin_clzll(ob);
-                    const uint32_t a = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, fa, y, z));
-                    const uint32_t b = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, fb, y, z) + 1);
-                    scan_run(gp, a, b, qx, qy, qz, wyz, t2, prm.lin, ns);
-                }
-#else
                 const uint32_t a = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, x, y, z));
                 const uint32_t b = lsm_ld(cs, lsm_cell_lin(G.nbx, G.nby, xe, y, z) + 1);
                 if (b > a) scan_run(gp, a, b, qx, qy, qz, wyz, t2, prm.lin, ns);
-#endif
                 x = xe + 1;
             }
         }
@@ -804,11 +790,6 @@ __device__ __forceinline__ void flush_stats(const NNStat &ls, unsigned long long
     }
 }
 
-template <int METHOD>
-__device__ __forceinline__ void accumulate_block(const PairState &P, const CloudDev &S,
-                                                 const CloudDev &G, int i, int idx, int32_t slot,
-                                                 double *__restrict__ partials);
-
 // LSM_NN_WPE=<w>: cap the correspondence kernel's registers for w waves per SIMD. 8 (64 VGPRs,
 // 2-4 registers spilled outside the walks) since the walks read the target through a buffer
 // descriptor: nn 81.7 -> 73.9 ms per step (7 waves: 76.1; round 2, with 64-bit addresses, the
@@ -825,21 +806,14 @@ __device__ __forceinline__ void accumulate_block(const PairState &P, const Cloud
 #else
 #define LSM_NN_ATTR
 #endif
-// FUSE (LSM_FUSE_ACC, passes >= 1): 1 + the estimation method -- a workgroup none of whose
-// queries went to the fallback also sums its block's partials (accumulate_block: the accumulate
-// kernel's arithmetic and fixed-order reduction, so the sums are bit-identical) while its source
-// and target points are cache-hot, and marks the block in `fused` (written for every block of
-// the plan: 1 fused, 0 left to the accumulate kernel).
-template <bool CHECK, bool STATS = false, int FUSE = 0>
+template <bool CHECK, bool STATS = false>
 __global__ void __launch_bounds__(NN_THREADS) LSM_NN_ATTR
 nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
           NNParams prm, int pass, const double *__restrict__ hist, int32_t *__restrict__ corr,
           int2 *__restrict__ rec, FallbackItem *__restrict__ queue,
           uint32_t *__restrict__ queue_n, uint32_t queue_cap, uint32_t *__restrict__ searched,
           unsigned long long *__restrict__ stats = nullptr,
-          const uint8_t *__restrict__ tiled = nullptr, double *__restrict__ partials = nullptr,
-          uint8_t *__restrict__ fused = nullptr) {
-    static_assert(!(FUSE && STATS), "statistics builds run the unfused kernels");
+          const uint8_t *__restrict__ tiled = nullptr) {
     // after nn_tile_kernel (same grid and plan): only the workgroups it did not tile
     if (tiled && tiled[blockIdx.x]) return;
     NNStat ls{};
@@ -863,12 +837,6 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         __shared__ int32_t s_idx[NN_THREADS];
         __shared__ float s_m[NN_THREADS];
         __shared__ int32_t s_cnt[NN_THREADS / LSM_WAVE];
-        __shared__ int32_t s_res[FUSE ? NN_THREADS : 1];   // searched queries' results (slot)
-        __shared__ int32_t s_pend;
-        const int own_i = i;
-        const bool own_live = live;
-        int own_slot = -1;
-        if (FUSE && threadIdx.x == 0) s_pend = 0;
         bool need = false;
         if (live)
             need = !check_query(P, S, G, i, P.src_off + i, prm, corr, rec,
@@ -887,7 +855,6 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
             const int slot = before + __popcll(bm & ((uint64_t(1) << lane) - 1));
             s_idx[slot] = i;
             s_m[slot] = m;
-            own_slot = slot;
         }
         __syncthreads();
         if (threadIdx.x == 0 && total > 0) atomicAdd(searched, uint32_t(total));
@@ -905,9 +872,8 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         // the highest wave boundary that still fits them); 2 as 0 with the query order reversed
         const int span = total * L;
         const int base = prm.split_place == 1 ? ((NN_THREADS - span) / LSM_WAVE) * LSM_WAVE : 0;
-        // a wave with nothing to search retires (no stats), unless it must join the fused
-        // accumulation (its lanes' queries: rel < 0 or q >= total below, so `live` is false)
-        if (!FUSE && ((w + 1) * LSM_WAVE <= base || w * LSM_WAVE >= base + span)) return;
+        if ((w + 1) * LSM_WAVE <= base || w * LSM_WAVE >= base + span)
+            return;   // this wave has nothing to search (no stats)
         const int rel = int(threadIdx.x) - base;
         int q = rel / L;
         live = rel >= 0 && q < total;
@@ -931,25 +897,10 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         if (lead) {
             corr[g] = pending ? -2 : result;
             if (!pending) rec[g] = rec_pack(a2, pass, r);
-            if (FUSE) {
-                s_res[q] = pending ? -2 : result;
-                if (pending) s_pend = 1;
-            }
         }
         if (STATS) {
             if (sub != 0) ls.v[0] = 0;   // one search per query
             flush_stats(ls, stats);
-        }
-        if constexpr (FUSE != 0) {
-            __syncthreads();
-            const bool go = s_pend == 0;
-            if (threadIdx.x == 0) fused[task.slot] = go ? 1 : 0;
-            if (!go) return;   // a fallback query: the accumulate kernel sums this block
-            // own query's neighbour: this lane's certified check left it in corr (its own
-            // write or the previous pass's), a searched one comes back through s_res
-            const int idx = !own_live ? -1 : (own_slot >= 0 ? s_res[own_slot]
-                                                            : corr[P.src_off + own_i]);
-            accumulate_block<FUSE - 1>(P, S, G, own_i, idx, task.slot, partials);
         }
         return;
     }
@@ -971,12 +922,6 @@ nn_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restr
         if (!pending) rec[g] = rec_pack(a2, pass, r);
     }
     if (STATS) flush_stats(ls, stats);
-    if constexpr (FUSE != 0) {
-        const bool any_pending = __syncthreads_or(pending);
-        if (threadIdx.x == 0) fused[task.slot] = any_pending ? 0 : 1;
-        if (any_pending) return;
-        accumulate_block<FUSE - 1>(P, S, G, i, live ? result : -1, task.slot, partials);
-    }
 }
 
 // The passes that search every query (nn_kernel<false>'s work) with LQ lanes per query: the rows
@@ -1784,19 +1729,23 @@ __device__ __forceinline__ double acc_value(int k, const double (&J)[6], double 
     return 0.0;
 }
 
-// One block's partial sums (a workgroup of NN_THREADS lanes, every lane calls it): lane i of the
-// block contributes the correspondence (source point i, target point idx; idx < 0 or i >= S.n:
-// nothing). Fixed-order reduction, so the sums do not depend on which kernel runs it: the
-// accumulate kernel (idx from corr) or, fused, the correspondence kernel that just found idx.
 template <int METHOD>
-__device__ __forceinline__ void accumulate_block(const PairState &P, const CloudDev &S,
-                                                 const CloudDev &G, int i, int idx, int32_t slot,
-                                                 double *__restrict__ partials) {
+__device__ __forceinline__ void accumulate_task(const BlockTask task,
+                                                const PairState *__restrict__ st,
+                                                const CloudDev *__restrict__ cds,
+                                                const int32_t *__restrict__ corr,
+                                                double *__restrict__ partials) {
+    const PairState &P = st[task.pair];
+    if (!P.active) return;
+    const CloudDev S = cds[P.src];
+    const CloudDev G = cds[P.tgt];
+    const int i = task.start + threadIdx.x;
     // the correspondence's terms; an invalid lane contributes zeros
     double J[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, sv[3] = {0.0, 0.0, 0.0}, tv[3] = {0.0, 0.0, 0.0};
     double r = 0.0, e2 = 0.0;
     bool valid = false;
     if (i < S.n) {
+        const int idx = corr[P.src_off + i];
         if (idx >= 0) {
             valid = true;
             double x, y, z;
@@ -1843,36 +1792,19 @@ __device__ __forceinline__ void accumulate_block(const PairState &P, const Cloud
         double s = 0.0;
 #pragma unroll
         for (int q = 0; q < NN_THREADS / LSM_WAVE; ++q) s += red[q][threadIdx.x];
-        partials[size_t(slot) * LSM_ACC + threadIdx.x] = s;
+        partials[size_t(task.slot) * LSM_ACC + threadIdx.x] = s;
     }
 }
 
 template <int METHOD>
-__device__ __forceinline__ void accumulate_task(const BlockTask task,
-                                                const PairState *__restrict__ st,
-                                                const CloudDev *__restrict__ cds,
-                                                const int32_t *__restrict__ corr,
-                                                double *__restrict__ partials) {
-    const PairState &P = st[task.pair];
-    if (!P.active) return;
-    const CloudDev S = cds[P.src];
-    const CloudDev G = cds[P.tgt];
-    const int i = task.start + threadIdx.x;
-    accumulate_block<METHOD>(P, S, G, i, i < S.n ? corr[P.src_off + i] : -1, task.slot, partials);
-}
-
-// fused (nullable): blocks the correspondence kernel already summed (nn_kernel FUSE)
-template <int METHOD>
 __global__ void __launch_bounds__(NN_THREADS)
 accumulate_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
-                  const int32_t *__restrict__ corr, double *__restrict__ partials,
-                  const uint8_t *__restrict__ fused = nullptr) {
+                  const int32_t *__restrict__ corr, double *__restrict__ partials) {
     for (int t = blockIdx.x;; t += gridDim.x) {
         BlockTask task;
         const int r = plan_task(tp, st, t, task);
         if (r < 0) break;
-        if (r > 0 && !(fused && fused[task.slot]))
-            accumulate_task<METHOD>(task, st, cds, corr, partials);
+        if (r > 0) accumulate_task<METHOD>(task, st, cds, corr, partials);
         __syncthreads();   // the task's LDS reduction buffer is reused by the next task
     }
 }
@@ -1969,22 +1901,11 @@ __global__ void __launch_bounds__(LSM_WAVE)
 solve_kernel(PairState *__restrict__ st, const double *__restrict__ partials, NNParams prm,
              int pass, const double *__restrict__ pair_bytes, uint32_t *__restrict__ active_next,
              double *__restrict__ bytes_next, unsigned long long *__restrict__ src_next,
-             int32_t *__restrict__ flags, double *__restrict__ hist,
-             const uint8_t *__restrict__ fused = nullptr, double *__restrict__ fused_bytes = nullptr) {
+             int32_t *__restrict__ flags, double *__restrict__ hist) {
     PairState &P = st[blockIdx.x];
     if (!P.active) return;
     __shared__ double tot[32];
     const int lane = threadIdx.x;
-    if (fused) {
-        // the correspondence pass's fused residual / JtJ work (SURVEY.md 8d B_res = N_s (12 + 4 +
-        // 24) bytes): source points of this pair's blocks that nn_kernel summed itself
-        uint32_t pts = 0;
-        for (int b = lane; b < P.nblk; b += LSM_WAVE)
-            if (fused[P.blk0 + b]) pts += uint32_t(min(NN_THREADS, P.nsrc - b * NN_THREADS));
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) pts += __shfl_xor(pts, off, LSM_WAVE);
-        if (lane == 0 && pts) atomicAdd(fused_bytes, 40.0 * double(pts));
-    }
     // lane l sums blocks l, l+64, ... for every component; then a fixed-tree wave reduction per
     // component (deterministic for a given block count)
     double part[30];
@@ -2209,7 +2130,6 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     uint32_t *d_counters = (uint32_t *)ctx->buf("i_counters", size_t(ncnt) * 4 * 4);
     double *d_bytes = (double *)ctx->buf("i_bytes", size_t(ncnt) * 8);
     unsigned long long *d_srcn = (unsigned long long *)ctx->buf("i_srcn", size_t(ncnt) * 8);
-    double *d_fbytes = (double *)ctx->buf("i_fbytes", size_t(ncnt) * 8);   // fused B_res per pass
     int32_t *d_pref = (int32_t *)ctx->buf("i_pref", size_t(npairs + 1) * 4);
     int64_t nblk_all = 0;
     for (int64_t k = 0; k < npairs; ++k) nblk_all += ps[k].nblk;
@@ -2217,8 +2137,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     int32_t *d_plan = (int32_t *)ctx->buf("i_plan", size_t(ncnt + 1) * 2 * 4);
     int32_t *d_flags = (int32_t *)ctx->buf("i_flags", size_t(std::max<int64_t>(npairs, 1)) * 4);
     int32_t *d_err = (int32_t *)ctx->buf("i_err", 4);
-    if (!d_corr || !d_rec || !d_q || !d_bq || !d_part || !d_counters || !d_bytes || !d_srcn ||
-        !d_fbytes || !d_pref ||
+    if (!d_corr || !d_rec || !d_q || !d_bq || !d_part || !d_counters || !d_bytes || !d_srcn || !d_pref ||
         !d_plan || !d_flags || !d_err || !d_coarse) {
         ctx->set_error("scratch allocation failed (icp)");
         return LSM_ENOMEM;
@@ -2231,7 +2150,6 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_err, 0, 4, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_bytes, 0, size_t(ncnt) * 8, st));
     LSM_HIP_TRY(ctx, hipMemsetAsync(d_srcn, 0, size_t(ncnt) * 8, st));
-    LSM_HIP_TRY(ctx, hipMemsetAsync(d_fbytes, 0, size_t(ncnt) * 8, st));
     if (src_off > 0) {
         LSM_HIP_TRY(ctx, hipMemsetAsync(d_corr, 0xff, size_t(src_off) * 4, st));
         LSM_HIP_TRY(ctx, hipMemsetAsync(d_rec, 0xff, size_t(src_off) * 8, st));
@@ -2331,18 +2249,6 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     const bool tile_search = lsm_knob("LSM_NN_TILE", 0) != 0.0;
     // LSM_NN_FULL_L: lanes per query in the passes that search every query (1, 2 or 4)
     const int full_l = int(lsm_knob("LSM_NN_FULL_L", 1));
-    // LSM_FUSE_ACC (default 1): from pass 1 on (the normals' side-stream refine has been joined
-    // by pass 0's accumulation) the correspondence kernel sums the partials of every block with
-    // no fallback query itself (nn_kernel FUSE; bit-identical, test_fused_accumulate_bit_identical)
-    const bool fuse_acc = lsm_knob("LSM_FUSE_ACC", 1) != 0.0 && !tile_search && full_l == 1;
-    uint8_t *d_fused = nullptr;
-    if (fuse_acc) {
-        d_fused = (uint8_t *)ctx->buf("i_fused", size_t(std::max(slot, 1)));
-        if (!d_fused) {
-            ctx->set_error("scratch allocation failed: i_fused");
-            return LSM_ENOMEM;
-        }
-    }
     double ms0 = 0.0;
     for (const char *k : {"nn", "nn_fallback"}) ms0 += ctx->stats[k].ms;
     unsigned long long *d_nst = nullptr;
@@ -2380,8 +2286,6 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         }
         if (done) break;
         hipEvent_t ev;
-        // pass 0 reads no normals before its accumulation joins the side stream: never fused
-        const bool fused_pass = fuse_acc && pass >= 1 && !d_nst;
         ctx->tic("nn", &ev);
         if (d_nst) {
             unsigned long long *sp = d_nst + size_t(pass) * NN_NSTAT;
@@ -2406,25 +2310,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         else if ((pass < CERT_FROM || nocert) && full_l == 4)
             nn_full_kernel<4><<<grid, NN_THREADS * 4, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_corr,
                                                                d_rec, d_q, d_qn + pass, qcap);
-        else if (fused_pass && (pass < CERT_FROM || nocert)) {
-            if (p.method == LSM_P2PLANE)
-                nn_kernel<false, false, 1 + LSM_P2PLANE><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap,
-                    d_sqn + pass, nullptr, nullptr, d_part, d_fused);
-            else
-                nn_kernel<false, false, 1 + LSM_P2P><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap,
-                    d_sqn + pass, nullptr, nullptr, d_part, d_fused);
-        } else if (fused_pass) {
-            if (p.method == LSM_P2PLANE)
-                nn_kernel<true, false, 1 + LSM_P2PLANE><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap,
-                    d_sqn + pass, nullptr, nullptr, d_part, d_fused);
-            else
-                nn_kernel<true, false, 1 + LSM_P2P><<<grid, NN_THREADS, 0, st>>>(
-                    tp, d_ps, d_cd, prm, pass, d_hist, d_corr, d_rec, d_q, d_qn + pass, qcap,
-                    d_sqn + pass, nullptr, nullptr, d_part, d_fused);
-        } else if (pass < CERT_FROM || nocert)
+        else if (pass < CERT_FROM || nocert)
             nn_kernel<false><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, prm, pass, d_hist, d_corr,
                                                                 d_rec, d_q, d_qn + pass, qcap,
                                                                 d_sqn + pass);
@@ -2470,19 +2356,17 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         // the normals' side-stream refine (pre-processing or the lazy targets above) has
         // overlapped this pass's correspondence search; the accumulation reads the normals
         ctx->join_side_device();
-        const uint8_t *fz = fused_pass ? d_fused : nullptr;
         if (p.method == LSM_P2PLANE)
             accumulate_kernel<LSM_P2PLANE><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, d_corr,
-                                                                        d_part, fz);
+                                                                        d_part);
         else
             accumulate_kernel<LSM_P2P><<<grid, NN_THREADS, 0, st>>>(tp, d_ps, d_cd, d_corr,
-                                                                    d_part, fz);
+                                                                    d_part);
         ctx->toc("accumulate", ev);
         ctx->tic("solve", &ev);
         solve_kernel<<<int(npairs), LSM_WAVE, 0, st>>>(d_ps, d_part, prm, pass, d_pbytes,
                                                        d_active + pass, d_bytes + pass,
-                                                       d_srcn + pass, d_flags, d_hist, fz,
-                                                       d_fbytes + pass);
+                                                       d_srcn + pass, d_flags, d_hist);
         ctx->toc("solve", ev);
         plan_kernel<<<1, PLAN_THREADS, 0, st>>>(d_ps, int(npairs), d_pref, d_coarse, d_plan,
                                                 d_active + pass, d_poll + 3 * pass);
@@ -2524,10 +2408,6 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
         LSM_HIP_TRY(ctx, hipMemcpy(hb.data(), d_bytes, size_t(passes) * 8, hipMemcpyDeviceToHost));
         nn_bytes = bytes0;   // pass 0: every pair
         for (int k = 0; k + 1 < passes; ++k) nn_bytes += hb[size_t(k)];
-        // the fused passes' residual / JtJ bytes (their kernel time includes that work)
-        std::vector<double> fb(size_t(passes) + 1, 0.0);
-        LSM_HIP_TRY(ctx, hipMemcpy(fb.data(), d_fbytes, size_t(passes) * 8, hipMemcpyDeviceToHost));
-        for (int k = 0; k < passes; ++k) nn_bytes += fb[size_t(k)];
         if (ctx->timing) {   // source points searched: all of them, then the active pairs'
             std::vector<unsigned long long> sn(size_t(passes), 0ull);
             LSM_HIP_TRY(ctx, hipMemcpy(sn.data(), d_srcn, size_t(passes) * 8,

@@ -37,10 +37,6 @@ struct CloudDev {
     const float4 *prior_ref;    // prior normals in reference order (orientation), or nullptr
     const double *xyz64;        // f64 coordinates in reference order (a voxelised cloud's f64
                                 // centroids: what Open3D's cloud holds), or nullptr
-    const uint64_t *rocc;       // row occupancy: word lin >> LSM_BLKX_SHIFT (one row of a layout
-                                // block), bit x & (LSM_BLKX - 1) set when cell x holds points
-                                // (grid_fill). The walks skip empty row parts without reading the
-                                // cell table: a block's 16 rows share one 128-B line
 };
 
 #define LSM_XYZ_PAD 16     // spare float4 points allocated past every processed cloud's end
@@ -53,8 +49,7 @@ struct CloudDev {
 #ifndef LSM_BLKX_SHIFT
 #define LSM_BLKX_SHIFT 6
 #endif
-static_assert(LSM_BLKX_SHIFT >= 2 && LSM_BLKX_SHIFT <= 6,
-              "x block width 4 .. 64 cells (a row's occupancy is one 64-bit word)");
+static_assert(LSM_BLKX_SHIFT >= 2 && LSM_BLKX_SHIFT <= 8, "x block width 4 .. 256 cells");
 #define LSM_BLKX (1 << LSM_BLKX_SHIFT)
 #define LSM_BLK_CELLS (LSM_BLKX * LSM_BLK * LSM_BLK)
 
@@ -183,24 +178,6 @@ struct BufPts {
 __device__ __forceinline__ BufPts cloud_buf_pts(const CloudDev &C) {
     return BufPts{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(C.xyz), 0,
                                                     (C.n + LSM_XYZ_PAD) * 16, 0x00020000)};
-}
-
-// LSM_ROCC (build option, default 1): the NN box search and the normals' ball walks test a row
-// part's occupancy word before reading the cell table (0: the cell table for every row part; the
-// same runs either way)
-#ifndef LSM_ROCC
-#define LSM_ROCC 1
-#endif
-// Occupied cells of row part [x, xe] (one layout block: x >> LSM_BLKX_SHIFT == xe >> ...) of row
-// (y, z): a mask of the row's x bits; the first / last occupied cell narrow the part without
-// changing its point run (the cells cut off hold no points).
-__device__ __forceinline__ uint64_t lsm_row_bits(const uint64_t *rocc, int nbx, int nby, int x,
-                                                 int xe, int y, int z) {
-    const uint64_t w = lsm_ld(rocc, size_t(uint32_t(lsm_cell_lin(nbx, nby, x, y, z)) >> LSM_BLKX_SHIFT));
-    const int lo = x & (LSM_BLKX - 1), hi = xe & (LSM_BLKX - 1);
-    const uint64_t m = (hi == 63 ? ~uint64_t(0) : ((uint64_t(1) << (hi + 1)) - 1)) &
-                       ~((uint64_t(1) << lo) - 1);
-    return w & m;
 }
 
 __device__ __forceinline__ int lsm_clampi(int v, int lo, int hi) {

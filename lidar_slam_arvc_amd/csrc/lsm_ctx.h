@@ -28,8 +28,6 @@ struct Cloud {
     int64_t cell_cap = 0;
     uint32_t *d_bmask = nullptr;  // block occupancy bits (the fallback's empty-block test)
     int64_t bmask_cap = 0;        // words
-    uint64_t *d_rocc = nullptr;   // row occupancy words (CloudDev::rocc)
-    int64_t rocc_cap = 0;         // words
     double *d_vox = nullptr;      // voxel centroids (f64, voxel-key order), voxelised clouds only
     int32_t *d_vkeys = nullptr;   // voxel keys (int32 x 3)
     int64_t vox_cap = 0;

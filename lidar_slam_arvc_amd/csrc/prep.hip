@@ -533,11 +533,9 @@ __device__ __forceinline__ uint32_t lower_bound_cell(const uint64_t *k, uint32_t
 
 __global__ void __launch_bounds__(FILL_THREADS)
 grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const *cell_out,
-          uint32_t *const *bm_out, uint64_t *const *rocc_out, uint32_t *nonempty) {
+          uint32_t *const *bm_out, uint32_t *nonempty) {
     static_assert(FILL_THREADS == 256 && FILL_TILE % LSM_BLK_CELLS == 0, "virtual-block bits");
-    static_assert(FILL_PER == 16, "row occupancy from 16-cell thread parts");
     __shared__ uint32_t tile[FILL_TILE];
-    __shared__ uint16_t occ16[FILL_THREADS];
     __shared__ uint32_t bounds[2];
     __shared__ uint32_t wmin[FILL_THREADS / LSM_WAVE];
     __shared__ uint32_t vbits[FILL_THREADS / LSM_WAVE];
@@ -602,30 +600,6 @@ grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const
         __syncthreads();
         for (int e = threadIdx.x; e < FILL_TILE; e += FILL_THREADS)
             if (c0 + e < c1) out[c0 + e] = tile[e];
-        // row occupancy words (CloudDev::rocc): cell e holds points iff the next start is later
-        {
-            const uint32_t nxt = threadIdx.x + 1 < FILL_THREADS ? tile[(threadIdx.x + 1) * FILL_PER]
-                                                               : p1;
-            uint32_t bits = 0;
-#pragma unroll
-            for (int i = 0; i < FILL_PER; ++i)
-                bits |= uint32_t((i + 1 < FILL_PER ? v[i + 1] : nxt) > v[i]) << i;
-            occ16[threadIdx.x] = uint16_t(bits);
-            __syncthreads();
-            constexpr int ROWS = FILL_TILE / LSM_BLKX;
-            if (threadIdx.x < ROWS && c0 + int64_t(threadIdx.x) * LSM_BLKX < int64_t(G.ncells)) {
-                const int cb = int(threadIdx.x) * LSM_BLKX;   // first cell of the row in the tile
-                uint64_t w = 0;
-                if (LSM_BLKX >= 16) {
-#pragma unroll
-                    for (int q = 0; q < (LSM_BLKX >= 16 ? LSM_BLKX / 16 : 1); ++q)
-                        w |= uint64_t(occ16[cb / 16 + q]) << (16 * q);
-                } else {
-                    w = (uint64_t(occ16[cb / 16]) >> (cb % 16)) & ((uint64_t(1) << LSM_BLKX) - 1);
-                }
-                rocc_out[c][(c0 >> LSM_BLKX_SHIFT) + threadIdx.x] = w;
-            }
-        }
         // occupancy bits of the tile's 64 virtual blocks (4x4x4 cells; bit v = layout block
         // v >> (LSM_BLKX_SHIFT - 2), x-chunk v & (LSM_BLKX / 4 - 1)): thread t tests the x-chunks
         // of block t / 4's four cell rows at z offset t % 4
@@ -826,23 +800,10 @@ __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, fl
             int x = xlo;
             while (x <= xhi) {
                 const int xe = min(xhi, x | (LSM_BLKX - 1));   // end of this block's row part
-                // empty parts end at the row's occupancy word; occupied ones narrow to their
-                // occupied cells (the same run) before the cell table
-#if LSM_ROCC
-                const uint64_t ob = lsm_row_bits(C.rocc, C.nbx, C.nby, x, xe, y, z);
-                if (ob) {
-                    const int xb0 = x & ~(LSM_BLKX - 1);
-                    const int l0 = lsm_cell_lin(C.nbx, C.nby, xb0 + __builtin_ctzll(ob), y, z);
-                    const int l1 = lsm_cell_lin(C.nbx, C.nby, xb0 + 63 - __builtin_clzll(ob), y, z);
-                    const uint32_t a = lsm_ld(C.cell_start, l0), b = lsm_ld(C.cell_start, l1 + 1);
-                    f(a, b, xl, xh);
-                }
-#else
                 const int l0 = lsm_cell_lin(C.nbx, C.nby, x, y, z);
                 const int l1 = lsm_cell_lin(C.nbx, C.nby, xe, y, z);
                 const uint32_t a = lsm_ld(C.cell_start, l0), b = lsm_ld(C.cell_start, l1 + 1);
                 if (b > a) f(a, b, xl, xh);
-#endif
                 x = xe + 1;
             }
         }
@@ -2477,7 +2438,6 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     }
     std::vector<CloudDev> cdev(K);
     std::vector<uint32_t *> perm_ptrs(K), cell_ptrs(K), bm_ptrs(K);
-    std::vector<uint64_t *> rocc_ptrs(K);
     for (int k = 0; k < K; ++k) {
         Cloud *c = clouds[k];
         if ((rc = ensure_cloud_buffers(ctx, c, wn[k], p.want_normals != 0))) return rc;
@@ -2501,20 +2461,9 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 return LSM_ENOMEM;
             }
         }
-        const int64_t rw = ncells >> LSM_BLKX_SHIFT;   // a word per block row
-        if (c->rocc_cap < rw || !c->d_rocc) {
-            (void)hipFree(c->d_rocc);
-            c->d_rocc = nullptr;
-            c->rocc_cap = rw;
-            if (hipMalloc(&c->d_rocc, size_t(std::max<int64_t>(rw, 1)) * 8) != hipSuccess) {
-                ctx->set_error("hipMalloc failed (row occupancy)");
-                return LSM_ENOMEM;
-            }
-        }
         CloudDev &D = cdev[k];
         D.xyz = c->d_xyz;
         D.bmask = c->d_bmask;
-        D.rocc = c->d_rocc;
         D.nrm = p.want_normals ? c->d_nrm : nullptr;
         D.cell_start = c->d_cell;
         D.ox = geo[k].ox;
@@ -2536,14 +2485,11 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         perm_ptrs[k] = c->d_perm;
         cell_ptrs[k] = c->d_cell;
         bm_ptrs[k] = c->d_bmask;
-        rocc_ptrs[k] = c->d_rocc;
     }
     GridGeo *d_geo;
     CloudDev *d_cd;
     uint32_t **d_perm_ptrs, **d_cell_ptrs, **d_bm_ptrs;
-    uint64_t **d_rocc_ptrs;
     if ((rc = upload_vec(ctx, "g_bmp", bm_ptrs, &d_bm_ptrs))) return rc;
-    if ((rc = upload_vec(ctx, "g_roccp", rocc_ptrs, &d_rocc_ptrs))) return rc;
     if ((rc = upload_vec(ctx, "g_geo", geo, &d_geo))) return rc;
     if ((rc = upload_vec(ctx, "g_cd", cdev, &d_cd))) return rc;
     if ((rc = upload_vec(ctx, "g_perm", perm_ptrs, &d_perm_ptrs))) return rc;
@@ -2582,7 +2528,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     {
         const int gx = int(std::min<int64_t>((maxcells1 + FILL_TILE - 1) / FILL_TILE, 4096));
         grid_fill<<<dim3(gx, K), FILL_THREADS, 0, st>>>(d_geo, K, k_out, d_cell_ptrs, d_bm_ptrs,
-                                                        d_rocc_ptrs, nonempty);
+                                                        nonempty);
     }
     ctx->toc("grid", ev);
 

@@ -205,12 +205,6 @@ def test_grid_layout_invariants(dev, seq64k, voxel):
             assert cells[0] == 0 and cells[-1] == n and np.all(np.diff(cells.astype(np.int64)) >= 0)
             sp = pts[perm]
             occ = np.flatnonzero(np.diff(cells.astype(np.int64)) > 0)
-            # row occupancy words: bit x of row word r <=> cell r * BLKX + x holds points
-            words = dev.row_occupancy(h)
-            nonempty = np.diff(cells.astype(np.int64)) > 0
-            assert len(words) * 64 == len(nonempty)   # LSM_BLKX = 64 cells per row
-            bits = np.unpackbits(words.view(np.uint8), bitorder="little").astype(bool)
-            assert np.array_equal(bits, nonempty)
             for c in occ:
                 a, b = int(cells[c]), int(cells[c + 1])
                 x = sp[a:b, 0]
@@ -499,34 +493,6 @@ def test_search_path_variants_bit_identical(dev, env, monkeypatch):
             assert a["fitness"] == b["fitness"] and a["inlier_rmse"] == b["inlier_rmse"]
             assert a["iterations"] == b["iterations"]
         assert np.array_equal(c_ref, c_got)
-    finally:
-        _release(dev, ids)
-
-
-@pytest.mark.parametrize("method", ["p2plane", "p2p"])
-def test_fused_accumulate_bit_identical(dev, monkeypatch, method):
-    """LSM_FUSE_ACC (default on): from pass 1 on, the correspondence kernel sums the partials of
-    every block none of whose queries went to the fallback (full and certified passes), the
-    accumulate kernel the rest. The same arithmetic and fixed-order reduction, so every result
-    equals the unfused run (LSM_FUSE_ACC=0) bit for bit: bench-sequence pairs (mostly fused
-    blocks) and revisit pairs (many fallback queries: mixed blocks), every pass."""
-    seq = synthetic.make_sequence(9, seed=3, model=synthetic.HDL64)
-    ps = synthetic.make_revisit_pairs(4, seed=41, model=synthetic.HDL64)
-    ids = _prep(dev, seq.scans + ps.targets + ps.sources)
-    try:
-        src = ids[1:9] + ids[13:17]
-        tgt = ids[0:8] + ids[9:13]
-        init = np.concatenate([seq.priors, ps.init])
-        prm = _lib.icp_params(method=method)
-        got = dev.icp_batch_arrays(src, tgt, init, prm)
-        c_got = dev.last_correspondences()
-        monkeypatch.setenv("LSM_FUSE_ACC", "0")
-        ref = dev.icp_batch_arrays(src, tgt, init, prm)
-        c_ref = dev.last_correspondences()
-        monkeypatch.delenv("LSM_FUSE_ACC")
-        _assert_batch_equal(ref, got)
-        assert np.array_equal(c_ref, c_got)
-        assert int(np.max(ref["iterations"])) > 2
     finally:
         _release(dev, ids)
 
