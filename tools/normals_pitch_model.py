@@ -71,6 +71,7 @@ class AnisoGrid:
         qx, qy, qz = q[:, 0] - self.o[0], q[:, 1] - self.o[1], q[:, 2] - self.o[2]
         prune = rad * 1.0001 + 1e-6
         rows = np.zeros(n, np.int64)
+        visited = np.zeros(n, np.int64)   # row parts the walk visits (slab-pruned), empty or not
         parts = np.zeros(n, np.int64)
         esearch = np.zeros(n, np.float64)
         steps = np.zeros(n, np.float64)
@@ -103,6 +104,7 @@ class AnisoGrid:
                 win = self.count(row, qx - ch, qx + ch)
                 before = self.count(row, cxl, qx - ch) - (win > 0) * 0
                 rows += live
+                visited += np.where(ok, nparts, 0)
                 parts += np.where(live, nparts, 0)
                 inwin += np.where(live, win, 0)
                 # entry search: runs of > BSEARCH points, 4-ary rounds down to SLACK points
@@ -112,7 +114,8 @@ class AnisoGrid:
                 esearch += np.where(live, rounds, 0)
                 slack = np.where(long_run, np.minimum(before, SLACK / 2.0), before)
                 steps += np.where(live, win + slack + 1.0, 0)
-        return dict(rows=rows, parts=parts, entry_rounds=esearch, steps=steps, in_window=inwin)
+        return dict(rows=rows, parts=parts, visited_parts=visited, entry_rounds=esearch,
+                    steps=steps, in_window=inwin)
 
 
 def model_scan(pts, pitches, nn_src=None):
@@ -151,6 +154,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scans", type=int, default=3)
     ap.add_argument("--json", default="")
+    ap.add_argument("--measured", default="",
+                    help="normals ms per C3 step at isotropic cells, e.g. 0.25=118.3,0.3=113.2,"
+                         "0.375=118.2,0.45=128.0 (bench.py --grid-cell)")
     args = ap.parse_args()
     from lidar_slam_arvc_amd import synthetic
     from oracle import cpu_ref as C
@@ -199,6 +205,9 @@ def main():
                                                            b["final_dense"]["parts"])
         er = (1 - df) * e["scan1_sparse"]["entry_rounds"] + df * (
             e["scan1_dense"]["entry_rounds"] + e["final_dense"]["entry_rounds"])
+        vs = (1 - df) * e["scan1_sparse"]["visited_parts"] + df * (
+            e["scan1_dense"]["visited_parts"] + e["final_dense"]["visited_parts"])
+        e["visited_row_parts_per_point"] = vs
         e["steps_per_point"] = st
         e["row_setups_per_point"] = rs
         e["entry_rounds_per_point"] = er
@@ -211,9 +220,27 @@ def main():
         print(f"{key:>18}: steps/pt {e['steps_per_point']:7.1f} ({e['steps_vs_0375']:.3f}x)  "
               f"row setups/pt {e['row_setups_per_point']:5.1f} ({e['row_setups_vs_0375']:.2f}x)  "
               f"entry rounds/pt {e['entry_rounds_per_point']:5.1f}  "
+              f"visited parts/pt {e['visited_row_parts_per_point']:5.1f}  "
               f"dense s1 {e['scan1_dense']['steps']:6.1f} fin {e['final_dense']['steps']:6.1f}  "
               f"nn rows {e['nn_box_rows_mean']:.2f} ({e['nn_rows_vs_0375']:.2f}x)  "
               f"cells {e['cells_per_cloud_padded'] / 1e6:.1f} M")
+    if args.measured:
+        # normals ms per C3 step measured at isotropic grid cells (bench.py --grid-cell): fit
+        # t = c0 + a * steps + b * visited row parts (per point), then predict every pitch
+        meas = {float(k): float(v) for k, v in (kv.split("=") for kv in args.measured.split(","))}
+        iso = [(c, summ[f"{c}/{c}/{c}"]) for c in sorted(meas) if f"{c}/{c}/{c}" in summ]
+        A = np.array([[1.0, e["steps_per_point"], e["visited_row_parts_per_point"]] for _, e in iso])
+        y = np.array([meas[c] for c, _ in iso])
+        coef, *_ = np.linalg.lstsq(A, y, rcond=None)
+        fit = {"normals_ms_per_step_measured": meas, "coef": {"c0": coef[0], "per_step": coef[1],
+                                                             "per_visited_part": coef[2]},
+               "step_equivalents_per_visited_part": coef[2] / coef[1] if coef[1] else None,
+               "residuals_ms": (A @ coef - y).tolist(),
+               "predicted_normals_ms": {k: float(coef[0] + coef[1] * e["steps_per_point"] +
+                                                 coef[2] * e["visited_row_parts_per_point"])
+                                        for k, e in summ.items()}}
+        res["calibration"] = fit
+        print(json.dumps(fit, indent=1))
     if args.json:
         with open(args.json, "w") as f:
             json.dump(res, f, indent=1)
