@@ -559,7 +559,7 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     // warm start: the previous pass's nearest neighbour bounds this pass's search. The search
     // stays exact -- the (d2, index) minimum over all points does not depend on the start.
     if (prev >= 0 && prev < G.n) t2 = top3_init(prev, sqd(lsm_ld(G.xyz, prev), qx, qy, qz), m);
-    const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
+    const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell_y,
                 fz = (qz - G.oz) * G.inv_cell;
     // a query outside the target's box searches around the nearest cell of the box: the
     // box faces that lie on the grid boundary bound nothing (no points beyond them)
@@ -596,17 +596,20 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
         NN_ST(ns, 6, 1);
     }
     NN_ST(ns, 5, K);
+    // K cells of `cell` in x and z; in y the same extent in the finer y cells (LSM_YSUB)
+    const int Ky = K * LSM_YSUB;
     const int x0 = max(cx - K, 0), x1 = min(cx + K, G.nx - 1);
-    const int y0 = max(cy - K, 0), y1 = min(cy + K, G.ny - 1);
+    const int y0 = max(cy - Ky, 0), y1 = min(cy + Ky, G.ny - 1);
     const int z0 = max(cz - K, 0), z1 = min(cz + K, G.nz - 1);
     const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
+    const float c2y = G.cell_y * G.cell_y * 0.9999f;
     const uint32_t *cs = G.cell_start;
     typedef typename std::conditional<GBUF, BufPts, GlobalPts>::type Rd;
     const Rd gp = [&]() {
         if constexpr (GBUF) return cloud_buf_pts(G);
         else return GlobalPts{G.xyz};
     }();
-    const int W = 2 * K + 1;
+    const int W = 2 * K + 1, Wy = 2 * Ky + 1;
     // Rows are visited centre-out (offsets 0, -1, 1, -2, 2, ...: |offset| never decreases) and
     // a row at offset d in z (or y) is at least (|d| - 1) cells from the query's slab. Once that
     // bound reaches the pruning radius (which only shrinks) every later row of the loop would
@@ -622,13 +625,13 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
         const float wz = slab_cells2(fz, z) * c2;
         if (wz >= t2.lim) continue;
 #pragma unroll 1
-        for (int iy = (sub - iz * W) & (L - 1); iy < W; iy += L) {   // rows t == sub (mod L)
+        for (int iy = (sub - iz * Wy) & (L - 1); iy < Wy; iy += L) {   // rows t == sub (mod L)
             const int ady = (iy + 1) >> 1;
-            if (ady >= 2 && wz + float((ady - 1) * (ady - 1)) * c2 >= t2.lim) break;
+            if (ady >= 2 && wz + float((ady - 1) * (ady - 1)) * c2y >= t2.lim) break;
             const int dy = (iy & 1) ? -ady : ady;
             const int y = cy + dy;
             if (y < y0 || y > y1) continue;
-            const float wyz = wz + slab_cells2(fy, y) * c2;
+            const float wyz = wz + slab_cells2(fy, y) * c2y;
             const float lim = t2.lim;
             if (wyz >= lim) continue;
             NN_ST(ns, 1, 1);
@@ -656,11 +659,11 @@ __device__ __forceinline__ bool nn_query(const double *T, const CloudDev &S, con
     // hold no points.
     const float bx = fminf(cx - K > 0 ? fx - float(cx - K) : INFINITY,
                            cx + K + 1 < G.nx ? float(cx + K + 1) - fx : INFINITY);
-    const float by = fminf(cy - K > 0 ? fy - float(cy - K) : INFINITY,
-                           cy + K + 1 < G.ny ? float(cy + K + 1) - fy : INFINITY);
+    const float by = fminf(cy - Ky > 0 ? fy - float(cy - Ky) : INFINITY,
+                           cy + Ky + 1 < G.ny ? float(cy + Ky + 1) - fy : INFINITY);
     const float bz = fminf(cz - K > 0 ? fz - float(cz - K) : INFINITY,
                            cz + K + 1 < G.nz ? float(cz + K + 1) - fz : INFINITY);
-    const float bound = fminf(bx, fminf(by, bz)) * G.cell;
+    const float bound = fminf(fminf(bx, bz) * G.cell, by * G.cell_y);
     const float bound2 = bound * bound * 0.99999f;
     if (L > 1) group_top3(t2, L);
     if (!(t2.bd2 <= bound2 || bound >= prm.maxc)) NN_ST(ns, 7, sub == 0 ? 1 : 0);
@@ -1076,7 +1079,7 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
         qy = float(y);
         qz = float(z);
     }
-    const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell,
+    const float fx = (qx - G.ox) * G.inv_cell, fy = (qy - G.oy) * G.inv_cell_y,
                 fz = (qz - G.oz) * G.inv_cell;
     auto clampc = [](float f, int n) { return (int)fminf(fmaxf(floorf(f), 0.f), float(n - 1)); };
     if (live && G.n > 0) {
@@ -1090,7 +1093,8 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
                   lq ? -cy : INT_MAX, lq ? cz : INT_MAX, lq ? -cz : INT_MAX};
     wg_min6(ext, red);
     const int x0 = max(ext[0] - NN_TMARGIN, 0), x1 = min(-ext[1] + NN_TMARGIN, G.nx - 1);
-    const int y0 = max(ext[2] - NN_TMARGIN, 0), y1 = min(-ext[3] + NN_TMARGIN, G.ny - 1);
+    const int y0 = max(ext[2] - NN_TMARGIN * LSM_YSUB, 0),
+              y1 = min(-ext[3] + NN_TMARGIN * LSM_YSUB, G.ny - 1);
     const int z0 = max(ext[4] - NN_TMARGIN, 0), z1 = min(-ext[5] + NN_TMARGIN, G.nz - 1);
     const bool boxed = G.n > 0 && x0 <= x1 && y0 <= y1 && z0 <= z1;   // some query is live
     const int nyb = boxed ? y1 - y0 + 1 : 0, nzb = boxed ? z1 - z0 + 1 : 0;
@@ -1197,10 +1201,11 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
                                y1 + 1 < G.ny ? float(y1 + 1) - fy : INFINITY);
         const float bz = fminf(z0 > 0 ? fz - float(z0) : INFINITY,
                                z1 + 1 < G.nz ? float(z1 + 1) - fz : INFINITY);
-        const float bound = fminf(bx, fminf(by, bz)) * G.cell;
+        const float bound = fminf(fminf(bx, bz) * G.cell, by * G.cell_y);
         const float bound2 = bound * bound * 0.99999f;
         const float cap2 = bound * bound * 1.0001f + 1e-6f;   // >= bound2 (f32 slack)
         const float c2 = G.cell * G.cell * 0.9999f;   // slack: cells assigned by f32 floor
+        const float c2y = G.cell_y * G.cell_y * 0.9999f;
         const int mz = max(cz - z0, z1 - cz), my = max(cy - y0, y1 - cy);
 #pragma unroll 1
         for (int iz = 0; iz <= 2 * mz; ++iz) {
@@ -1213,11 +1218,11 @@ nn_tile_kernel(TaskPlan tp, const PairState *__restrict__ st, const CloudDev *__
 #pragma unroll 1
             for (int iy = 0; iy <= 2 * my; ++iy) {
                 const int ady = (iy + 1) >> 1;
-                if (ady >= 2 && wz + float((ady - 1) * (ady - 1)) * c2 >= fminf(t2.lim, cap2))
+                if (ady >= 2 && wz + float((ady - 1) * (ady - 1)) * c2y >= fminf(t2.lim, cap2))
                     break;
                 const int y = cy + ((iy & 1) ? -ady : ady);
                 if (y < y0 || y > y1) continue;
-                const float wyz = wz + slab_cells2(fy, y) * c2;
+                const float wyz = wz + slab_cells2(fy, y) * c2y;
                 if (wyz >= fminf(t2.lim, cap2)) continue;
                 const int row = (z - z0) * nyb + (y - y0);
                 const uint32_t a = p_off[row * np], b = p_off[(row + 1) * np];
@@ -1396,6 +1401,9 @@ __device__ __forceinline__ void group_top2(Top2 &t) {
     t.lim = prune2(t.bd2, t.sd2, t.m);
 }
 
+// fewest fallback lanes per query: one per row range of a virtual block
+constexpr int FB_GL_MIN = LSM_BLKX == 4 || LSM_VB_ROWS <= 16 ? 16 : LSM_VB_ROWS;
+
 #ifndef LSM_FB_U
 #define LSM_FB_U 4        // candidate chunks per round (4 x 32: the whole first shell)
 #endif
@@ -1436,15 +1444,17 @@ fallback_run(const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
         transform_point(P.T, lsm_ld(S.xyz, q.i), qx64, qy64, qz64);
         const float qx = float(qx64), qy = float(qy64), qz = float(qz64);
         Top2 t2 = top2_init(q.best, q.best_d2, q.second_d2, q.margin);
-        // virtual blocks of 4x4x4 cells: one layout block holds 1 << VBS of them side by side in x;
-        // a virtual block is NR point ranges (its x-chunk of each of its 16 cell rows; one range
-        // when the layout block is itself 4 cells wide)
+        // virtual blocks of 4 x LSM_BLKY x 4 cells (cubes of edge 4 cell): one layout block holds
+        // 1 << VBS of them side by side in x; a virtual block is NR point ranges (its x-chunk of
+        // each of its LSM_VB_ROWS cell rows; one range when the layout block is 4 cells wide)
         constexpr int VBS = LSM_BLKX_SHIFT - 2;
-        constexpr int NR = LSM_BLKX == 4 ? 1 : 16;
+        constexpr int NR = LSM_BLKX == 4 ? 1 : LSM_VB_ROWS;
         constexpr int RL = LSM_BLKX == 4 ? LSM_BLK_CELLS : 4;   // cells per range
+        static_assert(NR == 1 || GL >= NR, "a lane per range");
+        constexpr bool BOTH = NR > 1 && GL < 2 * NR;   // each lane loads its range's start and end
         const int nvbx = G.nbx << VBS;
-        const float B = G.cell * float(LSM_BLK);   // virtual block edge
-        const float gx1 = G.ox + G.nx * G.cell, gy1 = G.oy + G.ny * G.cell,
+        const float B = G.cell * float(LSM_BLK);   // virtual block edge (= cell_y * LSM_BLKY)
+        const float gx1 = G.ox + G.nx * G.cell, gy1 = G.oy + G.ny * G.cell_y,
                     gz1 = G.oz + G.nz * G.cell;
         const float box2 = gap2(qx, G.ox, gx1) + gap2(qy, G.oy, gy1) + gap2(qz, G.oz, gz1);
         float fbound = 0.f;
@@ -1465,15 +1475,17 @@ fallback_run(const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
             auto outside = [](int v, int n) { return v < 0 ? -v : (v > n - 1 ? v - (n - 1) : 0); };
             const int r0 = max(outside(qbx, nvbx), max(outside(qby, G.nby), outside(qbz, G.nbz)));
             const uint32_t *cs = G.cell_start;
-            const int gl0 = grp * GL, rr = NR == 1 ? 0 : (sub & 15);
-            // this lane's cell-table words of a virtual block: range rr's start (sub & 16 == 0)
-            // or end; with 16-lane groups both
-            const int roff = (NR == 1 ? 0 : (rr >> 2) * 4 * LSM_BLKX + (rr & 3) * LSM_BLKX) +
-                             ((sub >> 4) & 1) * RL;
+            const int gl0 = grp * GL, rr = NR == 1 ? 0 : (sub & (NR - 1));
+            // this lane's cell-table words of a virtual block: range rr (row z rr / LSM_BLKY, y
+            // rr % LSM_BLKY)'s start (sub & NR == 0) or end; both when the group has fewer than
+            // 2 NR lanes
+            const int roff = (NR == 1 ? 0 : (rr / LSM_BLKY) * LSM_BLKY * LSM_BLKX +
+                                                (rr % LSM_BLKY) * LSM_BLKX) +
+                             (BOTH ? 0 : ((sub / NR) & 1) * RL);
             auto vb_word = [&](uint32_t vid) {
                 const size_t c = size_t(vid >> VBS) * LSM_BLK_CELLS +
                                  ((vid & ((1u << VBS) - 1u)) << 2) + uint32_t(roff);
-                return make_uint2(lsm_ld(cs, c), GL == 16 ? lsm_ld(cs, c + RL) : 0u);
+                return make_uint2(lsm_ld(cs, c), BOTH ? lsm_ld(cs, c + RL) : 0u);
             };
             int ra = r0, rb = r0 == 0 ? FB_R0 : r0;
             for (;;) {
@@ -1569,27 +1581,28 @@ fallback_run(const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
                             uint2 wn = w;
                             if (more) wn = vb_word(uint32_t(s_cand[u][src].x));
                             // the current block's ranges, each pruned by its rows' lower bound
-                            const uint32_t pa = GL == 16 ? w.x : __shfl(w.x, gl0 + rr, LSM_WAVE),
-                                           pb = GL == 16 ? w.y : __shfl(w.x, gl0 + 16 + rr, LSM_WAVE);
+                            const uint32_t pa = BOTH ? w.x : __shfl(w.x, gl0 + rr, LSM_WAVE),
+                                           pb = BOTH ? w.y : __shfl(w.x, gl0 + NR + rr, LSM_WAVE);
                             uint32_t n = pb - pa;
                             if (NR > 1) {
                                 const int4 cc = s_cand[u][csrc];
                                 const float cx = s_lbx[u][csrc];
-                                const int y = cc.z * 4 + (rr & 3), z = cc.w * 4 + (rr >> 2);
+                                const int y = cc.z * LSM_BLKY + (rr % LSM_BLKY),
+                                          z = cc.w * LSM_BLK + rr / LSM_BLKY;
                                 const float rlb =
-                                    cx + gap2(qy, G.oy + y * G.cell, G.oy + (y + 1) * G.cell) +
+                                    cx + gap2(qy, G.oy + y * G.cell_y, G.oy + (y + 1) * G.cell_y) +
                                     gap2(qz, G.oz + z * G.cell, G.oz + (z + 1) * G.cell);
                                 if (!(rlb * 0.9999f < lim0)) n = 0;
                             }
-                            uint32_t inc = n;   // inclusive prefix over the 16 ranges
+                            uint32_t inc = n;   // inclusive prefix over the NR ranges
                             if (NR > 1) {
 #pragma unroll
-                                for (int off = 1; off < 16; off <<= 1) {
-                                    const uint32_t o = __shfl_up(inc, off, 16);
+                                for (int off = 1; off < NR; off <<= 1) {
+                                    const uint32_t o = __shfl_up(inc, off, NR);
                                     if (rr >= off) inc += o;
                                 }
                             }
-                            const uint32_t T = NR > 1 ? __shfl(inc, gl0 + 15, LSM_WAVE) : n;
+                            const uint32_t T = NR > 1 ? __shfl(inc, gl0 + NR - 1, LSM_WAVE) : n;
                             const uint32_t ex = inc - n;
                             FB_ST(if (sub == 0) {
                                 fs[3] += 1;
@@ -1601,10 +1614,10 @@ fallback_run(const PairState *__restrict__ st, const CloudDev *__restrict__ cds,
                                 if (NR > 1) {   // the range holding point tt (all lanes shuffle)
                                     int lo = 0;
 #pragma unroll
-                                    for (int step = 8; step > 0; step >>= 1)
+                                    for (int step = NR / 2; step > 0; step >>= 1)
                                         if (__shfl(inc, gl0 + lo + step - 1, LSM_WAVE) <= tt)
                                             lo += step;
-                                    lo = min(lo, 15);
+                                    lo = min(lo, NR - 1);
                                     k = __shfl(pa, gl0 + lo, LSM_WAVE) +
                                         (tt - __shfl(ex, gl0 + lo, LSM_WAVE));
                                 }
@@ -2225,7 +2238,8 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
     // the fallback: GL lanes per queued query (LSM_FB_GL 16 / 32), LSM_FB_WAVES one-wave
     // workgroups per CU (grid-stride over the queue)
     // LSM_FB_GL 0 (default): chosen per pass on the device (nn_fallback_auto, LSM_FB_WIDE_MAX)
-    const int fb_gl = int(lsm_knob("LSM_FB_GL", 0));
+    // (16 lanes cannot hold a lane per range of a virtual block with more than 16 rows: 32 then)
+    const int fb_gl = int(lsm_knob("LSM_FB_GL", 0)) == 16 ? FB_GL_MIN : int(lsm_knob("LSM_FB_GL", 0));
     // whole-wave queries only where the fallback can search far: max_corr >= LSM_FB_WIDE_MAXC m
     // (C3 / C4's 10 m; a multi-scale ladder's <= 2 m searches are short and cheaper at 32 lanes)
     const uint32_t fb_wide_max =
@@ -2334,7 +2348,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                 // none) take a whole wave, the rest GL lanes
                 const float f2 = fb_far * fb_far;
                 if (gl == 16)
-                    nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                    nn_fallback_g<FB_GL_MIN><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
                                                                     qcap, d_corr, d_rec, pass, fst, f2, 0);
                 else
                     nn_fallback_g<32><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
@@ -2342,7 +2356,7 @@ int lsm_icp_run(lsm_ctx *ctx, int64_t npairs, Cloud **src, Cloud **tgt, const do
                 nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
                                                                 qcap, d_corr, d_rec, pass, fst, f2, 1);
             } else if (gl == 16)
-                nn_fallback_g<16><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
+                nn_fallback_g<FB_GL_MIN><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,
                                                                 qcap, d_corr, d_rec, pass, fst, INFINITY, 0);
             else if (gl == 64)
                 nn_fallback_g<64><<<fb_grid, LSM_WAVE, 0, st>>>(d_ps, d_cd, prm, d_q, d_qn + pass,

@@ -6,11 +6,13 @@
 //     grid row are ONE contiguous point range, and a workgroup of consecutive points covers a
 //     compact patch of space (coherent queries when the cloud is an ICP source);
 //   * a dense CSR cell table cell_start[ncells + 1] (u32) over the cloud's own bounding box, with
-//     cells linearised BLOCKED: LSM_BLKX x 4 x 4-cell blocks (x, y, z; 64 x 4 x 4 by default) in
-//     z-major order, cells z-major inside a block. A row of cells inside a block is one
-//     contiguous, x-sorted point range (what the walks scan), and a block's x-chunk of 4 cells
-//     in its 16 rows is a 4x4x4-cell virtual block (the coarse level the far-field search walks,
-//     with an occupancy bit each);
+//     cells linearised BLOCKED: LSM_BLKX x LSM_BLKY x 4-cell blocks (x, y, z; 64 x 8 x 4 by
+//     default) in z-major order, cells z-major inside a block. Cells are ANISOTROPIC: `cell` in x
+//     and z, cell / LSM_YSUB in y (0.375 x 0.1875 x 0.375 m by default), so a layout block is
+//     24 x 1.5 x 1.5 m. A row of cells inside a block is one contiguous, x-sorted point range
+//     (what the walks scan; its y width sets how much of a ball's disc a walk covers), and a
+//     block's x-chunk of 4 cells in its LSM_BLKY * 4 rows is a virtual block, a 1.5 m cube (the
+//     coarse level the far-field search walks, with an occupancy bit each);
 //   * normals float4 in the same order; perm[] maps sorted position -> reference (filter) order.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -26,12 +28,13 @@ struct CloudDev {
     const float4 *xyz;          // n, cell-sorted
     const float4 *nrm;          // n or nullptr
     const uint32_t *cell_start; // ncells + 1, offsets into xyz
-    const uint32_t *bmask;      // occupancy bit per virtual 4x4x4-cell block (id (bz*nby + by)*nvbx + vbx,
+    const uint32_t *bmask;      // occupancy bit per virtual block (4 x LSM_BLKY x 4 cells; id (bz*nby + by)*nvbx + vbx,
                                 //   nvbx = nbx * LSM_BLKX / 4; grid_fill)
     float ox, oy, oz;           // grid origin
-    float cell, inv_cell;       // cell edge and its reciprocal
+    float cell, inv_cell;       // cell edge in x and z and its reciprocal
+    float cell_y, inv_cell_y;   // cell edge in y (cell / LSM_YSUB) and its reciprocal
     int nx, ny, nz;             // cells per axis
-    int nbx, nby, nbz;          // layout blocks per axis (LSM_BLKX, 4, 4 cells)
+    int nbx, nby, nbz;          // layout blocks per axis (LSM_BLKX, LSM_BLKY, 4 cells)
     int n;
     const uint32_t *perm;       // sorted position -> reference order
     const float4 *prior_ref;    // prior normals in reference order (orientation), or nullptr
@@ -40,8 +43,16 @@ struct CloudDev {
 };
 
 #define LSM_XYZ_PAD 16     // spare float4 points allocated past every processed cloud's end
-#define LSM_BLK 4          // cells per block edge in y and z
+#define LSM_BLK 4          // cells per block edge in z (in y: LSM_BLKY)
 #define LSM_BLK_SHIFT 2
+// y cells are 1 / LSM_YSUB of the x / z cell edge (a walk covers
+// its ball's disc in rows as wide as a y cell; 0 = cubic cells)
+#ifndef LSM_YSUB_SHIFT
+#define LSM_YSUB_SHIFT 1
+#endif
+#define LSM_YSUB (1 << LSM_YSUB_SHIFT)
+#define LSM_BLKY_SHIFT (LSM_BLK_SHIFT + LSM_YSUB_SHIFT)
+#define LSM_BLKY (1 << LSM_BLKY_SHIFT)   // cells per block edge in y (the block stays 4 cells tall)
 // cells per block edge in x: 1 << LSM_BLKX_SHIFT (>= 2). A row of cells inside a block is one
 // contiguous, x-sorted run, so wider blocks cut the rows the walks visit into fewer runs
 // (64: C3 7670 -> 8561 pairs/s, profiles/r05o; the correspondence fallback keeps its own
@@ -51,15 +62,18 @@ struct CloudDev {
 #endif
 static_assert(LSM_BLKX_SHIFT >= 2 && LSM_BLKX_SHIFT <= 8, "x block width 4 .. 256 cells");
 #define LSM_BLKX (1 << LSM_BLKX_SHIFT)
-#define LSM_BLK_CELLS (LSM_BLKX * LSM_BLK * LSM_BLK)
+#define LSM_BLK_CELLS (LSM_BLKX * LSM_BLKY * LSM_BLK)
+// a virtual block: 4 x-cells of a layout block's LSM_VB_ROWS rows (a cube of edge 4 * cell)
+#define LSM_VB_ROWS (LSM_BLKY * LSM_BLK)
+#define LSM_VB_CELLS (4 * LSM_VB_ROWS)
 
 // blocked linear cell index (see layout note above): blocks z-major, then cells z-major inside
 // a block, x fastest
 __host__ __device__ __forceinline__ int lsm_cell_lin(int nbx, int nby, int x, int y, int z) {
-    const int bx = x >> LSM_BLKX_SHIFT, by = y >> LSM_BLK_SHIFT, bz = z >> LSM_BLK_SHIFT;
-    return (((bz * nby + by) * nbx + bx) << (LSM_BLKX_SHIFT + 2 * LSM_BLK_SHIFT)) |
-           ((z & (LSM_BLK - 1)) << (LSM_BLKX_SHIFT + LSM_BLK_SHIFT)) |
-           ((y & (LSM_BLK - 1)) << LSM_BLKX_SHIFT) | (x & (LSM_BLKX - 1));
+    const int bx = x >> LSM_BLKX_SHIFT, by = y >> LSM_BLKY_SHIFT, bz = z >> LSM_BLK_SHIFT;
+    return (((bz * nby + by) * nbx + bx) << (LSM_BLKX_SHIFT + LSM_BLKY_SHIFT + LSM_BLK_SHIFT)) |
+           ((z & (LSM_BLK - 1)) << (LSM_BLKX_SHIFT + LSM_BLKY_SHIFT)) |
+           ((y & (LSM_BLKY - 1)) << LSM_BLKX_SHIFT) | (x & (LSM_BLKX - 1));
 }
 
 // Per-pair ICP state (device). Layout kept 8-byte aligned.

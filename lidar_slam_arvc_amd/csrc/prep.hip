@@ -460,9 +460,10 @@ __global__ void point_cloud_ids(const uint32_t *cloud_off, const uint32_t *cloud
 // ------------------------------------------------------------------------------------------
 struct GridGeo {
     float ox, oy, oz, cell, inv_cell;
+    float cell_y, inv_cell_y;   // y cells: cell / LSM_YSUB
     int nx, ny, nz;
     int nbx, nby, nbz;
-    uint32_t cell_off;     // offset of this cloud in the global cell space
+    uint32_t cell_off;     // offset of this cloud in its sort group's cell key space (31 bits)
     uint32_t pt_off;       // offset of this cloud in the batch point arrays
     uint32_t n;
     uint32_t ncells;       // nbx * nby * nbz * LSM_BLK_CELLS (blocked, padded)
@@ -488,7 +489,7 @@ grid_keys(const Seg *segs, const float4 *pts, const GridGeo *geo, uint64_t *keys
     const uint32_t g = G.pt_off + i;
     float4 p = pts[g];
     int cx = cell_coord(p.x, G.ox, G.inv_cell, G.nx);
-    int cy = cell_coord(p.y, G.oy, G.inv_cell, G.ny);
+    int cy = cell_coord(p.y, G.oy, G.inv_cell_y, G.ny);
     int cz = cell_coord(p.z, G.oz, G.inv_cell, G.nz);
     // (cell, x) key: inside a cell points are ordered by x, which lets the correspondence search
     // walk a cell outwards from the query's x and stop once dx^2 exceeds the best distance
@@ -600,33 +601,44 @@ grid_fill(const GridGeo *geo, int ncloud, const uint64_t *skeys, uint32_t *const
         __syncthreads();
         for (int e = threadIdx.x; e < FILL_TILE; e += FILL_THREADS)
             if (c0 + e < c1) out[c0 + e] = tile[e];
-        // occupancy bits of the tile's 64 virtual blocks (4x4x4 cells; bit v = layout block
-        // v >> (LSM_BLKX_SHIFT - 2), x-chunk v & (LSM_BLKX / 4 - 1)): thread t tests the x-chunks
-        // of block t / 4's four cell rows at z offset t % 4
+        // occupancy bits of the tile's FILL_VB virtual blocks (4 x LSM_BLKY x 4 cells; bit v =
+        // layout block v >> VBS, x-chunk v & (LSM_BLKX / 4 - 1)): TPV threads per virtual block,
+        // thread t tests 4 of its rows (row r = 4 (t % TPV) + i: z r / LSM_BLKY, y r % LSM_BLKY)
         {
             constexpr int VBS = LSM_BLKX_SHIFT - 2;
-            const uint32_t vb = threadIdx.x >> 2, zi = threadIdx.x & 3;
-            const uint32_t v = uint32_t(c0 >> 6) + vb;
+            constexpr int FILL_VB = FILL_TILE / LSM_VB_CELLS;   // 64 (cubic cells) or 32
+            constexpr int TPV = FILL_THREADS / FILL_VB;          // 4 or 8
+            constexpr int BPW = LSM_WAVE / TPV;                  // virtual blocks per wave
+            static_assert(TPV * 4 == LSM_VB_ROWS && FILL_VB % 32 == 0, "virtual-block bits");
+            const uint32_t vb = threadIdx.x / TPV, ti = threadIdx.x % TPV;
+            const uint32_t v = uint32_t(c0 / LSM_VB_CELLS) + vb;
             const int64_t cell0 = int64_t(v >> VBS) * LSM_BLK_CELLS +
-                                  ((v & ((1u << VBS) - 1u)) << 2) + zi * 4 * LSM_BLKX - c0;
+                                  ((v & ((1u << VBS) - 1u)) << 2) - c0;
             bool occ = false;
 #pragma unroll
-            for (int yi = 0; yi < 4; ++yi) {
-                const int64_t e0 = cell0 + yi * LSM_BLKX, e1 = e0 + 4;
+            for (int i = 0; i < 4; ++i) {
+                const int r = int(ti) * 4 + i;
+                const int64_t e0 = cell0 + (r / LSM_BLKY) * LSM_BLKY * LSM_BLKX +
+                                   (r % LSM_BLKY) * LSM_BLKX, e1 = e0 + 4;
                 const uint32_t a = tile[e0], b = e1 < FILL_TILE ? tile[e1] : p1;
                 occ |= b > a;
             }
             uint64_t m = __ballot(occ);
-            m |= m >> 1;
-            m |= m >> 2;   // bit 4 j: block j of this wave's 16
+#pragma unroll
+            for (int sh = 1; sh < TPV; sh <<= 1) m |= m >> sh;   // bit TPV j: block j of the wave
             uint32_t bits = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) bits |= uint32_t((m >> (4 * j)) & 1u) << j;
+            for (int j = 0; j < BPW; ++j) bits |= uint32_t((m >> (TPV * j)) & 1u) << j;
             if (lane == 0) vbits[w] = bits;
             __syncthreads();
-            if (threadIdx.x < 2)
-                bm_out[c][(c0 >> 11) + threadIdx.x] =
-                    vbits[2 * threadIdx.x] | (vbits[2 * threadIdx.x + 1] << 16);
+            constexpr int WPT = FILL_VB / 32;   // bit-mask words per tile
+            if (threadIdx.x < WPT) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int q = 0; q < 32 / BPW; ++q)
+                    word |= vbits[threadIdx.x * (32 / BPW) + q] << (q * BPW);
+                bm_out[c][(c0 / FILL_TILE) * WPT + threadIdx.x] = word;
+            }
         }
         __syncthreads();
     }
@@ -785,7 +797,7 @@ template <typename F>
 __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, float r, F &&f) {
     int xlo, xhi, ylo, yhi, zlo, zhi;
     axis_range(qf.x, C.ox, C.inv_cell, r, C.nx, xlo, xhi);
-    axis_range(qf.y, C.oy, C.inv_cell, r, C.ny, ylo, yhi);
+    axis_range(qf.y, C.oy, C.inv_cell_y, r, C.ny, ylo, yhi);
     axis_range(qf.z, C.oz, C.inv_cell, r, C.nz, zlo, zhi);
     const float prune = r * 1.0001f + 1e-6f;
     const float prune2 = prune * prune;
@@ -793,7 +805,7 @@ __device__ __forceinline__ void ball_visit_runs(const CloudDev &C, float4 qf, fl
         const float dz2 = slab_d2(qf.z, C.oz, C.cell, z);
         if (dz2 > prune2) continue;
         for (int y = ylo; y <= yhi; ++y) {
-            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell, y);
+            const float dyz2 = dz2 + slab_d2(qf.y, C.oy, C.cell_y, y);
             if (dyz2 > prune2) continue;
             const float ch = sqrtf(prune2 - dyz2) * 1.0001f + 1e-6f * fabsf(qf.x) + 1e-5f;
             const float xl = qf.x - ch, xh = qf.x + ch;
@@ -1125,8 +1137,9 @@ __device__ __forceinline__ bool predict_dense(const CloudDev &C, const NormalPar
         return c < 0 ? 0 : (c > n - 1 ? n - 1 : c);
     };
     const int l = lsm_cell_lin(C.nbx, C.nby, cc(qf.x, C.ox, C.inv_cell, C.nx),
-                               cc(qf.y, C.oy, C.inv_cell, C.ny), cc(qf.z, C.oz, C.inv_cell, C.nz));
-    return float(lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l)) >= np.dense_k * C.cell * C.cell;
+                               cc(qf.y, C.oy, C.inv_cell_y, C.ny), cc(qf.z, C.oz, C.inv_cell, C.nz));
+    return float(lsm_ld(C.cell_start, l + 1) - lsm_ld(C.cell_start, l)) >=
+           np.dense_k * C.cell * C.cell_y;
 }
 
 // Phase statistics of hybrid_lane (diagnostics, normals_phase_kernel only): per lane, walk steps
@@ -2393,6 +2406,12 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     // ---------------- spatial grid ----------------
 
     std::vector<GridGeo> geo(K);
+    // The (cell, x) sort runs per group of consecutive clouds whose cells fit 31 bits: keys of
+    // at most 63 bits, 7 onesweep passes of 9 bits (a 2000-keyframe batch's cells need 32 bits
+    // with the finer y cells: one sort over all of it would take 8 passes)
+    constexpr uint64_t GROUP_CELLS = (uint64_t(1) << 31) - 2;
+    std::vector<int> gfirst{0};      // first cloud of every sort group
+    std::vector<uint64_t> gcells{0};  // cells of every group
     uint64_t cell_total = 0;
     const float cell_req = p.grid_cell > 0 ? float(p.grid_cell) : LSM_DEFAULT_GRID_CELL;
     for (int k = 0; k < K; ++k) {
@@ -2407,10 +2426,11 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
             for (int a = 0; a < 3; ++a) ext[a] = float(bb[6 * k + 3 + a] - bb[6 * k + a]);
             for (;;) {
                 const int64_t nx = int64_t(std::floor(ext[0] / c)) + 1;
-                const int64_t ny = int64_t(std::floor(ext[1] / c)) + 1;
+                const int64_t ny = int64_t(std::floor(ext[1] / (c / float(LSM_YSUB)))) + 1;
                 const int64_t nz = int64_t(std::floor(ext[2] / c)) + 1;
-                const int64_t padded = ((nx + LSM_BLKX - 1) / LSM_BLKX) * ((ny + 3) / 4) *
-                                       ((nz + 3) / 4) * LSM_BLK_CELLS;
+                const int64_t padded = ((nx + LSM_BLKX - 1) / LSM_BLKX) *
+                                       ((ny + LSM_BLKY - 1) / LSM_BLKY) * ((nz + 3) / 4) *
+                                       LSM_BLK_CELLS;
                 if (padded <= MAX_CELLS_PER_CLOUD) {
                     G.nx = int(nx);
                     G.ny = int(ny);
@@ -2425,16 +2445,20 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         }
         G.cell = c;
         G.inv_cell = 1.f / c;
+        G.cell_y = c / float(LSM_YSUB);      // exact: a power-of-two division
+        G.inv_cell_y = 1.f / G.cell_y;
         G.nbx = (G.nx + LSM_BLKX - 1) / LSM_BLKX;
-        G.nby = (G.ny + LSM_BLK - 1) / LSM_BLK;
+        G.nby = (G.ny + LSM_BLKY - 1) / LSM_BLKY;
         G.nbz = (G.nz + LSM_BLK - 1) / LSM_BLK;
         G.ncells = uint32_t(G.nbx) * G.nby * G.nbz * LSM_BLK_CELLS;
-        G.cell_off = uint32_t(cell_total);
-        cell_total += uint64_t(G.ncells);
-        if (cell_total >= (uint64_t(1) << 32) - 1) {
-            ctx->set_error("batch too large for the 32-bit cell key space; split the batch");
-            return LSM_EINVAL;
+        if (cell_total + uint64_t(G.ncells) + 1 > GROUP_CELLS) {   // a new sort group
+            gfirst.push_back(k);
+            gcells.push_back(0);
+            cell_total = 0;
         }
+        G.cell_off = uint32_t(cell_total);   // offset in the group's cell key space
+        cell_total += uint64_t(G.ncells);
+        gcells.back() = cell_total;
     }
     std::vector<CloudDev> cdev(K);
     std::vector<uint32_t *> perm_ptrs(K), cell_ptrs(K), bm_ptrs(K);
@@ -2451,7 +2475,7 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
                 return LSM_ENOMEM;
             }
         }
-        const int64_t bmw = ncells / 2048 + 2;   // a bit per 64 cells, whole fill tiles
+        const int64_t bmw = ncells / (32 * LSM_VB_CELLS) + 2;   // a bit per virtual block
         if (c->bmask_cap < bmw || !c->d_bmask) {
             (void)hipFree(c->d_bmask);
             c->d_bmask = nullptr;
@@ -2471,6 +2495,8 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
         D.oz = geo[k].oz;
         D.cell = geo[k].cell;
         D.inv_cell = geo[k].inv_cell;
+        D.cell_y = geo[k].cell_y;
+        D.inv_cell_y = geo[k].inv_cell_y;
         D.nx = geo[k].nx;
         D.ny = geo[k].ny;
         D.nz = geo[k].nz;
@@ -2515,13 +2541,33 @@ int lsm_prep_batch(lsm_ctx *ctx, std::vector<Cloud *> &clouds, const lsm_prep_pa
     for (int k = 0; k < K; ++k) maxcells1 = std::max<int64_t>(maxcells1, int64_t(geo[k].ncells) + 1);
     if (!psegs.empty()) {
         grid_keys<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, wpts, d_geo, k_in, v_in);
+        // one sort per group over its clouds' (contiguous) points
+        const int ng = int(gfirst.size());
+        auto grange = [&](int g, uint32_t &a, uint32_t &n) {
+            const int k0 = gfirst[size_t(g)], k1 = g + 1 < ng ? gfirst[size_t(g) + 1] : K;
+            a = woff[size_t(k0)];
+            n = woff[size_t(k1) - 1] + wn[size_t(k1) - 1] - a;
+        };
         size_t tmpb = 0;
-        const int endbit = 32 + bits_for(cell_total);
-        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<uint64_t>>(nullptr, tmpb, k_in, k_out, v_in, v_out,
-                                                                   size_t(ntot), 0, endbit, st));
+        for (int g = 0; g < ng; ++g) {
+            uint32_t a, n;
+            grange(g, a, n);
+            size_t b = 0;
+            LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<uint64_t>>(
+                                 nullptr, b, k_in + a, k_out + a, v_in + a, v_out + a, size_t(n), 0,
+                                 32 + bits_for(gcells[size_t(g)]), st));
+            tmpb = std::max(tmpb, b);
+        }
         void *tmp = ctx->buf("sort_tmp", tmpb);
-        LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<uint64_t>>(tmp, tmpb, k_in, k_out, v_in, v_out,
-                                                                   size_t(ntot), 0, endbit, st));
+        for (int g = 0; g < ng; ++g) {
+            uint32_t a, n;
+            grange(g, a, n);
+            if (n == 0) continue;
+            size_t b = tmpb;
+            LSM_HIP_TRY(ctx, rocprim::radix_sort_pairs<SortConfig<uint64_t>>(
+                                 tmp, b, k_in + a, k_out + a, v_in + a, v_out + a, size_t(n), 0,
+                                 32 + bits_for(gcells[size_t(g)]), st));
+        }
         grid_scatter<<<int(psegs.size()), PT_THREADS, 0, st>>>(d_psegs, d_geo, d_cd, v_out, wpts,
                                                               d_perm_ptrs);
     }
