@@ -65,7 +65,7 @@ typedef struct {
     int32_t want_normals;  /* 1 for 'icppointplane', 0 for 'icppointpoint';
                             * LSM_NORMALS_LAZY: normals on demand (below)                  */
     double grid_cell;      /* spatial-grid cell edge in x and z, metres (y cells: half of it);
-                            * <= 0 -> library default (0.375; voxelised clouds:
+                            * <= 0 -> library default (0.42; voxelised clouds:
                             * max(0.75, 2.5 voxel_size)) */
 } lsm_prep_params;
 

@@ -33,11 +33,13 @@ constexpr int FILTER_PER_THREAD = 4;
 constexpr int FILTER_CHUNK = FILTER_THREADS * FILTER_PER_THREAD;
 constexpr int PT_THREADS = 256;
 constexpr int64_t MAX_CELLS_PER_CLOUD = int64_t(1) << 24;
-// Default cell edge of the keyframe grid (m). Measured on the HDL-64 bench (pairs/s):
-// 0.3 4136, 0.36 4308, 0.4 4336, 0.45 4177, 0.5 4028 -- larger cells cost the normals walk
-// (rows of 0.09+ m^2 cross-section) and the NN row walks, smaller ones push far queries into
-// the fallback (4x4x4-cell blocks shrink with the cell).
-constexpr float LSM_DEFAULT_GRID_CELL = 0.375f;
+// Default cell edge of the keyframe grid in x and z (m; y cells are half of it). With cubic cells
+// (rounds 1-5) 0.375 m was best (round 1: 0.3 4136, 0.36 4308, 0.4 4336, 0.45 4177, 0.5 4028
+// pairs/s); with the anisotropic cells of round 6 (profiles/r06/gridcell_ysub_sweep.txt) C3 runs
+// 8727 / 9328 / 9445 pairs/s at 0.33 / 0.375 / 0.42 m and C4 6270 / 6995 / 7168 -- larger cells
+// cost the walks (wider row windows), smaller ones push far queries into the fallback (its
+// virtual blocks, 4 x-cells wide, shrink with the cell).
+constexpr float LSM_DEFAULT_GRID_CELL = 0.42f;
 constexpr float LSM_VOXEL_GRID_CELL_MIN = 0.75f;   // voxelised clouds (lsm_prep_batch)
 
 struct Seg {           // (keyframe, first point) of one workgroup

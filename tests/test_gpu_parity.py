@@ -212,8 +212,8 @@ def test_grid_layout_invariants(dev, seq64k, voxel):
                 assert np.all(dx >= 0)
                 assert np.all(np.diff(perm[a:b])[dx == 0] > 0)   # x ties in reference order
                 ext = sp[a:b].max(0) - sp[a:b].min(0)
-                # cells: c in x and z, c / 2 in y (c: 0.375 m, voxelised max(0.75, 2.5 voxel))
-                c = max(0.75, 2.5 * voxel) if voxel else 0.375
+                # cells: c in x and z, c / 2 in y (c: 0.42 m, voxelised max(0.75, 2.5 voxel))
+                c = max(0.75, 2.5 * voxel) if voxel else 0.42
                 assert np.all(ext <= np.array([c, c / 2, c]) * (1 + 1e-5)), ext
     finally:
         _release(dev, ids)
