@@ -104,6 +104,13 @@ void lsm_default_icp_params(lsm_icp_params *p);
 int lsm_cloud_upload(lsm_ctx *ctx, const float *xyz, int64_t n, lsm_cloud *out);
 /* Same from float64 (rounded to float32 on the device hot path). */
 int lsm_cloud_upload_f64(lsm_ctx *ctx, const double *xyz, int64_t n, lsm_cloud *out);
+/* `count` lsm_cloud_upload calls in one (the keyframes of a sequence, keyframemanager.py's
+ * load of every keyframe before pre_process): xyz[i] holds n[i] x 3 float32, out[i] receives its
+ * handle. One device allocation and one synchronisation for the batch (each cloud's points start
+ * 256-byte aligned in it; the allocation is freed with the batch's last handle). On an error no
+ * handle is created. */
+int lsm_cloud_upload_batch(lsm_ctx *ctx, const float *const *xyz, const int64_t *n, int64_t count,
+                           lsm_cloud *out);
 /* A second handle on a device copy of src's raw points (no host round trip), for processing one
  * scan at several settings at once: the multi-scale chain of config C5
  * keeps one voxelised cloud per scale, where the reference would call voxel_down_sample on

@@ -22,7 +22,7 @@ LSM_NORMALS_LAZY = 2     # lsm_prep_params.want_normals: normals on demand
 
 EXPORTED = [
     "lsm_init", "lsm_free", "lsm_last_error", "lsm_version", "lsm_default_prep_params",
-    "lsm_default_icp_params", "lsm_cloud_upload", "lsm_cloud_upload_f64", "lsm_cloud_clone", "lsm_cloud_release",
+    "lsm_default_icp_params", "lsm_cloud_upload", "lsm_cloud_upload_f64", "lsm_cloud_upload_batch", "lsm_cloud_clone", "lsm_cloud_release",
     "lsm_cloud_info", "lsm_preprocess", "lsm_preprocess_batch", "lsm_cloud_download",
     "lsm_cloud_voxel_keys", "lsm_cloud_layout", "lsm_icp", "lsm_icp_batch", "lsm_icp_last_correspondences",
     "lsm_loop_candidates", "lsm_loop_triplet_partners", "lsm_set_timing", "lsm_kernel_stats",
@@ -73,6 +73,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "lsm_default_icp_params": (None, [C.POINTER(IcpParams)]),
         "lsm_cloud_upload": (C.c_int, [_P, _f32p, C.c_int64, _i64p]),
         "lsm_cloud_upload_f64": (C.c_int, [_P, _f64p, C.c_int64, _i64p]),
+        "lsm_cloud_upload_batch": (C.c_int, [_P, C.POINTER(_f32p), _i64p, C.c_int64, _i64p]),
         "lsm_cloud_clone": (C.c_int, [_P, C.c_int64, _i64p]),
         "lsm_cloud_release": (C.c_int, [_P, C.c_int64]),
         "lsm_cloud_info": (C.c_int, [_P, C.c_int64, _i64p, _i64p, _i32p]),
@@ -197,6 +198,23 @@ class Device:
             self.check(self.lib.lsm_cloud_upload_f64(self.handle, _ptr(p, C.c_double), len(p),
                                                      C.byref(out)), "lsm_cloud_upload_f64")
         return out.value
+
+    def upload_many(self, clouds) -> list:
+        """lsm_cloud_upload_batch: every cloud (N x 3; float64 rounded to float32 on the host, as
+        lsm_cloud_upload_f64 does) in one device allocation and one synchronisation."""
+        arrs = []
+        for points in clouds:
+            p = np.asarray(points)
+            if p.ndim != 2 or p.shape[1] != 3:
+                raise ValueError("points must be N x 3")
+            arrs.append(np.ascontiguousarray(p, dtype=np.float32))
+        k = len(arrs)
+        ptrs = (_f32p * max(k, 1))(*[_ptr(a, C.c_float) for a in arrs])
+        ns = np.array([len(a) for a in arrs] or [0], dtype=np.int64)
+        out = np.zeros(max(k, 1), dtype=np.int64)
+        self.check(self.lib.lsm_cloud_upload_batch(self.handle, ptrs, _ptr(ns, C.c_int64), k,
+                                                   _ptr(out, C.c_int64)), "lsm_cloud_upload_batch")
+        return [int(x) for x in out[:k]]
 
     def clone(self, cloud: int) -> int:
         out = C.c_int64()

@@ -146,7 +146,10 @@ static Cloud *find_cloud(lsm_ctx *ctx, lsm_cloud id) {
 }
 
 static void free_cloud(Cloud *c) {
-    (void)hipFree(c->d_raw);
+    if (c->raw_slab)
+        c->raw_slab.reset();   // a batch upload's slice: the batch's allocation goes with its last cloud
+    else
+        (void)hipFree(c->d_raw);
     (void)hipFree(c->d_xyz);
     (void)hipFree(c->d_nrm);
     (void)hipFree(c->d_perm);
@@ -293,6 +296,55 @@ int lsm_cloud_upload(lsm_ctx *ctx, const float *xyz, int64_t n, lsm_cloud *out) 
 
 int lsm_cloud_upload_f64(lsm_ctx *ctx, const double *xyz, int64_t n, lsm_cloud *out) {
     return upload_common(ctx, xyz, n, true, out);
+}
+
+// Per-call costs dominate uploading many small scans one by one (an allocation, a copy and a
+// synchronisation each: ≈ 39 us per HDL-64 scan on top of the copy), so a batch
+// takes one allocation and one synchronisation, its copies queued back to back on the stream.
+int lsm_cloud_upload_batch(lsm_ctx *ctx, const float *const *xyz, const int64_t *n, int64_t count,
+                           lsm_cloud *out) {
+    if (!ctx || count < 0 || (count > 0 && (!xyz || !n || !out))) return LSM_EINVAL;
+    std::vector<size_t> off(static_cast<size_t>(count));
+    size_t total = 0;
+    for (int64_t i = 0; i < count; ++i) {
+        if (n[i] < 0 || (n[i] > 0 && !xyz[i])) return LSM_EINVAL;
+        if (n[i] >= (int64_t(1) << 31)) {
+            ctx->set_error("cloud too large (>= 2^31 points)");
+            return LSM_EINVAL;
+        }
+        off[size_t(i)] = total;
+        total += (size_t(n[i] > 0 ? n[i] : 1) * 12 + 255) / 256 * 256;
+    }
+    if (count == 0) return LSM_OK;
+    (void)hipSetDevice(ctx->device);
+    void *slab = nullptr;
+    if (hipMalloc(&slab, total) != hipSuccess) {
+        ctx->set_error("hipMalloc failed for a batch of raw clouds");
+        return LSM_ENOMEM;
+    }
+    std::shared_ptr<void> keep(slab, [](void *p) { (void)hipFree(p); });
+    char *base = static_cast<char *>(slab);
+    hipError_t e = hipSuccess;
+    for (int64_t i = 0; i < count && e == hipSuccess; ++i)
+        if (n[i] > 0)
+            e = hipMemcpyAsync(base + off[size_t(i)], xyz[i], size_t(n[i]) * 12,
+                               hipMemcpyHostToDevice, ctx->stream);
+    const hipError_t es = hipStreamSynchronize(ctx->stream);   // (also before a failed batch's free)
+    if (e == hipSuccess) e = es;
+    if (e != hipSuccess) {
+        ctx->set_error(std::string("lsm_cloud_upload_batch: ") + hipGetErrorString(e));
+        return LSM_EHIP;
+    }
+    for (int64_t i = 0; i < count; ++i) {
+        Cloud *c = new Cloud();
+        c->n_raw = n[i];
+        c->d_raw = reinterpret_cast<float *>(base + off[size_t(i)]);
+        c->raw_slab = keep;
+        const int64_t id = ctx->next_id++;
+        ctx->clouds[id] = c;
+        out[i] = id;
+    }
+    return LSM_OK;
 }
 
 int lsm_cloud_clone(lsm_ctx *ctx, lsm_cloud src, lsm_cloud *out) {

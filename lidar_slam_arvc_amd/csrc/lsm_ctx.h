@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -19,6 +20,8 @@ struct DevBuf {
 struct Cloud {
     int64_t n_raw = 0;
     float *d_raw = nullptr;       // n_raw x 3 float32 (as uploaded, reference order)
+    std::shared_ptr<void> raw_slab;   // lsm_cloud_upload_batch: the batch's allocation d_raw
+                                      // points into (freed with its last cloud), else null
     int64_t cap = 0;              // capacity of the processed arrays (points)
     int64_t n = 0;                // processed points
     float4 *d_xyz = nullptr;      // cell-sorted points

@@ -35,6 +35,47 @@ def _release(dev, ids):
         dev.release(i)
 
 
+# ------------------------------------------------------------------ boundary (8b)
+def test_batch_upload_matches_single_uploads(dev, seq64k):
+    """lsm_cloud_upload_batch (one allocation, one synchronisation for the batch) against one
+    lsm_cloud_upload per cloud: the same raw counts and, pre-processed, the same points and
+    normals bit for bit -- with an empty cloud, float64 input and an odd-sized cloud in the batch
+    (each slice 256-byte aligned); an empty batch; the batch's handles released one by one (its
+    allocation lives until the last) while the single uploads stay usable; an invalid count
+    creates no handle."""
+    import ctypes as C
+
+    rng = np.random.default_rng(8)
+    clouds = [seq64k.scans[0], np.zeros((0, 3), np.float32),
+              np.asarray(seq64k.scans[1], np.float64),
+              rng.uniform(-5.0, 5.0, (1001, 3)).astype(np.float32)]
+    prm = _lib.prep_params()
+    a = [dev.upload(c) for c in clouds]
+    b = dev.upload_many(clouds)
+    try:
+        assert dev.upload_many([]) == []
+        assert [dev.info(i)[0] for i in b] == [len(c) for c in clouds]
+        dev.preprocess(a, prm)
+        dev.preprocess(b, prm)
+        for x, y in zip(a, b):
+            px, nx = dev.download(x, normals=True)
+            py, ny = dev.download(y, normals=True)
+            assert np.array_equal(px, py) and np.array_equal(nx, ny)
+        for y in b[:2]:
+            dev.release(y)
+        dev.preprocess(b[2:], prm)
+        assert np.array_equal(dev.download(b[3])[0], dev.download(a[3])[0])
+        b = b[2:]
+        ns = np.array([-1], dtype=np.int64)
+        out = np.array([-7], dtype=np.int64)
+        ptrs = (C.POINTER(C.c_float) * 1)(clouds[0].ctypes.data_as(C.POINTER(C.c_float)))
+        rc = dev.lib.lsm_cloud_upload_batch(dev.handle, ptrs, ns.ctypes.data_as(
+            C.POINTER(C.c_int64)), 1, out.ctypes.data_as(C.POINTER(C.c_int64)))
+        assert rc != 0 and out[0] == -7
+    finally:
+        _release(dev, a + b)
+
+
 # ------------------------------------------------------------------ filter (a2)
 def test_filter_bit_exact(dev, seq64k):
     ids = _prep(dev, seq64k.scans, want_normals=False)
