@@ -160,7 +160,7 @@ class KeyFrame:
 
     def load_pointcloud(self):
         path = self.pcd_path()
-        if self._handle is not None and self._source == path:
+        if self.resident(path):
             return          # device keyframe cache: same file already resident
         self.set_points(read_pcd(path), source=path)
 
@@ -168,8 +168,18 @@ class KeyFrame:
         """Attach an in-memory N x 3 scan (float32 = PCD precision) instead of reading a file."""
         self._release()
         xyz = np.asarray(xyz)
-        self._handle = self._dev.upload(xyz if xyz.dtype == np.float32 else
-                                        np.asarray(xyz, dtype=np.float64))
+        self._attach(self._dev.upload(xyz if xyz.dtype == np.float32 else
+                                      np.asarray(xyz, dtype=np.float64)), xyz, source)
+
+    def resident(self, source) -> bool:
+        """the raw cloud of `source` (a path) is already on the device (keyframe cache)"""
+        return self._handle is not None and self._source == source
+
+    def _attach(self, handle, xyz, source):
+        """take over an uploaded raw cloud (set_points, KeyFrameManager.load_pointclouds)"""
+        self._release()
+        xyz = np.asarray(xyz)
+        self._handle = handle
         self._source = source
         self.pointcloud = HostPointCloud(np.asarray(xyz, dtype=np.float64))
         self.pointcloud_filtered = None

@@ -19,6 +19,7 @@ import numpy as np
 
 from . import _lib
 from .keyframe import HostPointCloud, KeyFrame
+from .pcd import read_pcd
 from .se3 import HomogeneousMatrix
 
 _OPTION = {"icppointpoint": "pointpoint", "icppointplane": "pointplane"}
@@ -44,8 +45,20 @@ class KeyFrameManager:
                                        voxel_size=self.voxel_size, device=self._dev))
 
     def load_pointclouds(self):
+        """keyframemanager.py:32-35. The scans not already resident are read, then uploaded as
+        one batch (lsm_cloud_upload_batch: one device allocation and one synchronisation; the
+        allocation is freed with the last of the batch's clouds, so unloading single keyframes
+        of a batch returns their memory only when the whole batch is unloaded)."""
+        todo = [kf for kf in self.keyframes
+                if kf._dev is self._dev and not kf.resident(kf.pcd_path())]
+        if todo:
+            xyzs = [read_pcd(kf.pcd_path()) for kf in todo]
+            for kf in todo:
+                kf._release()
+            for kf, xyz, h in zip(todo, xyzs, self._dev.upload_many(xyzs)):
+                kf._attach(h, xyz, kf.pcd_path())
         for kf in self.keyframes:
-            kf.load_pointcloud()
+            kf.load_pointcloud()     # keyframes on another device; no-op for the resident ones
 
     def load_pointcloud(self, i):
         self.keyframes[i].load_pointcloud()

@@ -60,6 +60,18 @@ def test_batch_api_equals_single(euroc):
     for k in range(3):
         single = kfm.compute_transformation(k, k + 1, pri[k])
         assert np.array_equal(single.array, batch[k].array)
+    # load_pointclouds: every scan in one lsm_cloud_upload_batch; the same registrations
+    kfm2 = KeyFrameManager(d, np.array(times), voxel_size=None, device=kfm._dev)
+    kfm2.add_keyframes(1)
+    kfm2.load_pointclouds()
+    assert all(kf._handle is not None for kf in kfm2.keyframes)
+    kfm2.load_pointclouds()                # resident: nothing re-read or re-uploaded
+    kfm2.pre_process_batch([0, 1, 2, 3])
+    batch2 = kfm2.compute_transformations([(0, 1), (1, 2), (2, 3)], pri)
+    for k in range(3):
+        assert np.array_equal(batch2[k].array, batch[k].array)
+    kfm2.unload_pointcloud(0)              # the batch's allocation lives on for the others
+    assert np.array_equal(kfm2.compute_transformation(1, 2, pri[1]).array, batch[1].array)
 
 
 def test_keyframe_voxel_and_filters(euroc):
