@@ -8,10 +8,11 @@
 //   * a dense CSR cell table cell_start[ncells + 1] (u32) over the cloud's own bounding box, with
 //     cells linearised BLOCKED: LSM_BLKX x LSM_BLKY x 4-cell blocks (x, y, z; 64 x 8 x 4 by
 //     default) in z-major order, cells z-major inside a block. Cells are ANISOTROPIC: `cell` in x
-//     and z, cell / LSM_YSUB in y (0.375 x 0.1875 x 0.375 m by default), so a layout block is
-//     24 x 1.5 x 1.5 m. A row of cells inside a block is one contiguous, x-sorted point range
-//     (what the walks scan; its y width sets how much of a ball's disc a walk covers), and a
-//     block's x-chunk of 4 cells in its LSM_BLKY * 4 rows is a virtual block, a 1.5 m cube (the
+//     and z, cell / LSM_YSUB in y (0.42 x 0.21 x 0.42 m by default; voxelised clouds
+//     max(0.75, 2.5 voxel) in x / z), so a layout block is 26.9 x 1.68 x 1.68 m. A row of cells
+//     inside a block is one contiguous, x-sorted point range (what the walks scan; its y width
+//     sets how much of a ball's disc a walk covers), and a block's x-chunk of 4 cells in its
+//     LSM_BLKY * 4 rows is a virtual block, a cube of edge 4 cells (1.68 m; the
 //     coarse level the far-field search walks, with an occupancy bit each);
 //   * normals float4 in the same order; perm[] maps sorted position -> reference (filter) order.
 #pragma once
