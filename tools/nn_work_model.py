@@ -25,8 +25,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CELL = np.float32(0.375)
-BLK = 4           # cells per layout block edge in y and z
+CELL = np.float32(0.375)   # x / z cell edge (--cell)
+YSUB = 1          # y cells are CELL / YSUB (--ysub; lsm_common.h LSM_YSUB: 2 since round 6)
+CELLY = CELL
+BLK = 4           # cells per layout block edge in z
+BLKY = 4          # ... in y (4 * YSUB)
 BLKX = 64         # ... and in x (lsm_common.h LSM_BLKX)
 LIN = 8            # runs of at most this many points are scanned whole
 KCOLD, KMAX = 4, 4
@@ -40,16 +43,18 @@ class Grid:
         p = pts.astype(np.float32)
         self.o = p.min(axis=0)
         self.inv = np.float32(1.0) / CELL
+        self.invy = np.float32(1.0) / CELLY
+        self.inv3 = np.array([self.inv, self.invy, self.inv], np.float32)
         ext = p.max(axis=0) - self.o
-        self.n = (np.floor(ext / CELL).astype(np.int64) + 1)
-        self.nb = (self.n + np.array([BLKX, BLK, BLK]) - 1) // np.array([BLKX, BLK, BLK])
-        c = np.floor((p - self.o) * self.inv).astype(np.int64)
+        self.n = (np.floor(ext * self.inv3).astype(np.int64) + 1)
+        self.nb = (self.n + np.array([BLKX, BLKY, BLK]) - 1) // np.array([BLKX, BLKY, BLK])
+        c = np.floor((p - self.o) * self.inv3).astype(np.int64)
         c = np.minimum(np.maximum(c, 0), self.n - 1)
         lin = self.lin(c[:, 0], c[:, 1], c[:, 2])
         order = np.lexsort((p[:, 0], lin))
         self.p = p[order]
         self.x = self.p[:, 0]
-        ncell = int(self.nb[0] * self.nb[1] * self.nb[2] * BLKX * BLK * BLK)
+        ncell = int(self.nb[0] * self.nb[1] * self.nb[2] * BLKX * BLKY * BLK)
         cnt = np.bincount(lin, minlength=ncell)
         self.cs = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
 
@@ -61,9 +66,16 @@ class Grid:
                 (z & 3) * 4 + (y & 3))
 
     def lin(self, x, y, z):
-        bx, by, bz = x // BLKX, y >> 2, z >> 2
-        return (((bz * self.nb[1] + by) * self.nb[0] + bx) * (BLKX * 16)) + ((z & 3) * 4 * BLKX) + \
-               ((y & 3) * BLKX) + (x % BLKX)
+        """lsm_cell_lin"""
+        bx, by, bz = x // BLKX, y // BLKY, z >> 2
+        return (((bz * self.nb[1] + by) * self.nb[0] + bx) * (BLKX * BLKY * BLK)) + \
+               ((z & 3) * BLKY * BLKX) + ((y % BLKY) * BLKX) + (x % BLKX)
+
+    def occ_line(self, x, y, z):
+        """the 128-B line of the 64-bit occupancy word of (y, z)'s row in x's layout block"""
+        blk = self.lin(x, y, z) // (BLKX * BLKY * BLK)
+        row = (z & 3) * BLKY + (y % BLKY)
+        return (blk * BLKY * BLK + row) * 8 // 128
 
 
 def sqd(t, q):
@@ -98,7 +110,7 @@ def query(G, q, prev, m, st):
     t2 = Top3(-1, INF, m)
     if prev >= 0:
         t2 = Top3(prev, sqd(G.p[prev], q), m)
-    f = (q - G.o) * G.inv
+    f = (q - G.o) * G.inv3
     c = [int(min(max(math.floor(f[a]), 0), G.n[a] - 1)) for a in range(3)]
     K = KCOLD
     if t2.bidx < 0:
@@ -110,10 +122,13 @@ def query(G, q, prev, m, st):
     elif t2.bd2 < INF:
         rc = math.sqrt(t2.bd2) * G.inv * 1.0001 + 1e-4
         K = KMAX if rc >= KMAX else max(1, math.ceil(rc))
-    lo = [max(c[a] - K, 0) for a in range(3)]
-    hi = [min(c[a] + K, G.n[a] - 1) for a in range(3)]
+    Ks = [K, K * YSUB, K]
+    lo = [max(c[a] - Ks[a], 0) for a in range(3)]
+    hi = [min(c[a] + Ks[a], G.n[a] - 1) for a in range(3)]
     c2 = float(CELL * CELL * np.float32(0.9999))
+    c2y = float(CELLY * CELLY * np.float32(0.9999))
     W = 2 * K + 1
+    Wy = 2 * K * YSUB + 1
 
     def slab(fv, k):
         d = k - fv if fv < k else (fv - (k + 1) if fv > k + 1 else 0.0)
@@ -130,15 +145,15 @@ def query(G, q, prev, m, st):
         wz = slab(f[2], z) * c2
         if wz >= t2.lim:
             continue
-        for iy in range(W):
+        for iy in range(Wy):
             ady = (iy + 1) >> 1
-            if ady >= 2 and wz + (ady - 1) ** 2 * c2 >= t2.lim:
+            if ady >= 2 and wz + (ady - 1) ** 2 * c2y >= t2.lim:
                 break
             y = c[1] + (-ady if iy & 1 else ady)
             st["row_iters"] += 1
             if y < lo[1] or y > hi[1]:
                 continue
-            wyz = wz + slab(f[1], y) * c2
+            wyz = wz + slab(f[1], y) * c2y
             lim = t2.lim
             if wyz >= lim:
                 continue
@@ -162,7 +177,7 @@ def query(G, q, prev, m, st):
                                         ("e", G.rb(xe, y, z) * 4 // 128)))
                     # occupancy bits: one 64-bit word per block row (x cells), the block's 16
                     # rows in one 128-B line; the cell table is read only for occupied parts
-                    LINES["occ"].add(("o", G.lin(x, y, z) // (BLKX * 16)))
+                    LINES["occ"].add(("o", G.occ_line(x, y, z)))
                     if b > a:
                         LINES["occ"].update((la * 4 // 128, lb * 4 // 128))
                         st["parts_nonempty"] += 1
@@ -256,7 +271,14 @@ def main():
     ap.add_argument("--pairs", type=int, default=2)
     ap.add_argument("--queries", type=int, default=16384, help="queries per pair (cell order)")
     ap.add_argument("--json", default="")
+    ap.add_argument("--cell", type=float, default=0.375, help="x / z cell edge (round 6: 0.42)")
+    ap.add_argument("--ysub", type=int, default=1, help="y cells per x / z cell (round 6: 2)")
     args = ap.parse_args()
+    global CELL, CELLY, YSUB, BLKY
+    CELL = np.float32(args.cell)
+    YSUB = args.ysub
+    CELLY = np.float32(args.cell / args.ysub)
+    BLKY = 4 * YSUB
     from lidar_slam_arvc_amd import synthetic
     from oracle import cpu_ref as C
     # rough VALU weights per counted iteration (icp.hip nn_query / scan_run)
